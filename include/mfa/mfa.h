@@ -1,0 +1,420 @@
+/*
+ * mfa.h — C ABI of the MI355X (gfx950 / CDNA4) fused-attention library.
+ *
+ * This is the drop-in boundary for the hot path of bghira/metal-flash-attention-plus
+ * (the reference; paths below are relative to its repository root).  Every entry point
+ * cites the Swift interface it replaces.  The reference dispatches Metal command buffers;
+ * here every launch enqueues onto a caller-provided hipStream_t (passed as void*) and
+ * returns without synchronising, which is the analogue of encoding into a caller command
+ * buffer (`MultiHeadAttention.encodeForward`, Sources/FlashAttention/Attention/
+ * MultiHeadAttention.swift:197-234).
+ *
+ * Conventions (identical to the reference kernels):
+ *   - All tensor pointers are DEVICE pointers owned by the caller (MTLBuffer analogue).
+ *   - Logical layout is BHSD ([batch, heads, seq, head_dim]); strides are ELEMENT strides in
+ *     BHSD order with the last dimension contiguous (MultiHeadAttention.swift:325-336).
+ *   - O, dQ, dK, dV are FP32 in memory (AttentionDescriptor+Precisions.swift:143-146).
+ *   - L (log-sum-exp) is stored in base-2 units premultiplied by log2(e):
+ *     L = m + log2(l)  (AttentionKernel+Caching.swift:394-400); FP16 when
+ *     low_precision_intermediates, else FP32.
+ *   - D = softmax_scale * rowsum(dO ∘ O)  (AttentionKernel+Softmax.swift:233); BF16
+ *     (upper 16 bits of the FP32 value) when low_precision_intermediates, else FP32.
+ *   - GQA/MQA kv head = head % num_kv_heads (AttentionKernel+Source.swift:80-86).
+ *
+ * Errors: every function returns mfa_status_t; mfa_last_error() gives a thread-local
+ * message.  The reference uses fatalError/precondition for invalid descriptors
+ * (AttentionDescriptor.swift:95, AttentionKernel.swift:45, GEMMQuantization.swift:198-208)
+ * and `nil`+print for pipeline failures (MultiHeadAttention.swift:44-47, :470-473).
+ */
+#ifndef MFA_MFA_H
+#define MFA_MFA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MFA_ABI_VERSION 1
+
+typedef enum mfa_status {
+  MFA_SUCCESS = 0,
+  MFA_ERR_INVALID_DESCRIPTOR = 1, /* fatalError("Descriptor was incomplete.") et al. */
+  MFA_ERR_UNSUPPORTED = 2,        /* configuration the kernels do not implement */
+  MFA_ERR_LAUNCH = 3,             /* hipLaunchKernel / runtime failure */
+  MFA_ERR_INVALID_ARGUMENT = 4,   /* null pointer / bad size */
+  MFA_ERR_NO_DEVICE = 5
+} mfa_status_t;
+
+/* GEMMOperandPrecision (Sources/FlashAttention/GEMM/GEMMOperandPrecision.swift:22-27),
+ * identical raw values. */
+typedef enum mfa_precision {
+  MFA_PRECISION_FP32 = 0,
+  MFA_PRECISION_FP16 = 1,
+  MFA_PRECISION_BF16 = 2,
+  MFA_PRECISION_INT8 = 3,
+  MFA_PRECISION_INT4 = 4,
+  MFA_PRECISION_UNSET = -1 /* Swift `nil` for inputMemoryPrecision (resolves to FP16) */
+} mfa_precision_t;
+
+/* AttentionKernelType (Attention/AttentionKernelType.swift:10-29). */
+typedef enum mfa_kernel_type {
+  MFA_KERNEL_FORWARD = 0,
+  MFA_KERNEL_BACKWARD_QUERY = 1,
+  MFA_KERNEL_BACKWARD_KEY_VALUE = 2,
+  MFA_KERNEL_MLA_COMPRESSED = 3
+} mfa_kernel_type_t;
+
+/* AttentionOperand (Attention/AttentionOperand.swift:9-24); buffer slots of
+ * AttentionOperand.bufferBinding (:50-67): Q0 K1 V2 O3 L4 D5 dO6 dV7 dK8 dQ9. */
+typedef enum mfa_operand {
+  MFA_OPERAND_Q = 0,
+  MFA_OPERAND_K = 1,
+  MFA_OPERAND_S = 2,
+  MFA_OPERAND_P = 3,
+  MFA_OPERAND_V = 4,
+  MFA_OPERAND_O = 5,
+  MFA_OPERAND_L = 6,
+  MFA_OPERAND_D = 7,
+  MFA_OPERAND_dO = 8,
+  MFA_OPERAND_dV = 9,
+  MFA_OPERAND_dP = 10,
+  MFA_OPERAND_dS = 11,
+  MFA_OPERAND_dK = 12,
+  MFA_OPERAND_dQ = 13,
+  MFA_OPERAND_COUNT = 14
+} mfa_operand_t;
+
+/* Returns the reference buffer slot of an operand, or -1 (AttentionOperand.swift:50-67). */
+int mfa_operand_buffer_binding(mfa_operand_t operand);
+
+/* SparsityPattern (AttentionDescriptor.swift:10-15). `custom` is accepted and treated as
+ * none, exactly as AttentionDescriptor.setFunctionConstants does (:226-229). */
+typedef enum mfa_sparsity {
+  MFA_SPARSITY_NONE = 0,
+  MFA_SPARSITY_CAUSAL = 1,
+  MFA_SPARSITY_SLIDING_WINDOW = 2,
+  MFA_SPARSITY_CUSTOM = 3
+} mfa_sparsity_t;
+
+/* SparseMaskDescriptor.MaskType (AttentionDescriptor.swift:47-51). */
+typedef enum mfa_mask_type {
+  MFA_MASK_DENSE = 0,         /* mask buffer = fp32 additive [B, H, R, C] added to QK^T */
+  MFA_MASK_SPARSE_RANGES = 1, /* mask buffer = uint32x2 [B, H_kv, R] half-open key ranges */
+  MFA_MASK_BLOCK_SPARSE = 2   /* flag only; ranges built by mfa_sparse_build_block_sparse */
+} mfa_mask_type_t;
+
+/* AttentionDescriptor (AttentionDescriptor.swift:17-43). */
+typedef struct mfa_attention_descriptor {
+  int32_t low_precision_inputs;          /* Q, K, V, dO */
+  int32_t input_memory_precision;        /* mfa_precision_t; MFA_PRECISION_UNSET = nil */
+  int32_t low_precision_intermediates;   /* S, P, L, D, dP, dS */
+  int32_t has_matrix_dimensions;         /* Optional matrixDimensions */
+  uint32_t row;                          /* output sequence length R */
+  uint32_t column;                       /* input sequence length C */
+  uint16_t head;                         /* head dimension D */
+  uint16_t reserved0;
+  int32_t has_transpose_state;           /* Optional transposeState */
+  int32_t transpose_q, transpose_k, transpose_v, transpose_o;
+  int32_t sparsity_pattern;              /* mfa_sparsity_t */
+  uint32_t window_size;                  /* slidingWindow(windowSize:) */
+  int32_t has_softmax_scale;             /* Optional softmaxScale; default 1/sqrt(D) */
+  float softmax_scale;
+  int32_t has_sparse_mask;               /* Optional sparseMask */
+  int32_t mask_type;                     /* mfa_mask_type_t */
+  int32_t block_sparse_block_size;
+  int32_t is_mqa;
+  uint32_t num_kv_heads;
+} mfa_attention_descriptor_t;
+
+/* Fills the Swift default-initialised descriptor (AttentionDescriptor.init, :45). */
+void mfa_attention_descriptor_init(mfa_attention_descriptor_t* desc);
+
+/* AttentionKernelDescriptor (AttentionKernelDescriptor.swift:8-66). */
+typedef struct mfa_kernel_descriptor {
+  uint16_t block_parallelization;  /* blockDimensions.parallelization */
+  uint16_t block_traversal;        /* blockDimensions.traversal */
+  uint16_t block_head;             /* blockDimensions.head */
+  uint16_t head_dimension;
+  uint32_t sequence_length;        /* max(R, C) */
+  int32_t cache_state[MFA_OPERAND_COUNT];          /* cached in registers? */
+  int32_t memory_precisions[MFA_OPERAND_COUNT];    /* mfa_precision_t or -1 */
+  int32_t register_precisions[MFA_OPERAND_COUNT];  /* mfa_precision_t or -1 */
+  int32_t transpose_state[MFA_OPERAND_COUNT];
+  int32_t prefer_async_cache;
+  int32_t prefer_async_load;
+  int32_t has_softmax_scale;
+  float softmax_scale;
+  int32_t type;                    /* mfa_kernel_type_t */
+  int32_t masking_strategy_override; /* -1 none, 0 elementWise, 1 bitmask */
+} mfa_kernel_descriptor_t;
+
+/* AttentionDescriptor.kernelDescriptor(type:) (AttentionDescriptor.swift:80-190) with the
+ * gfx950 parameter table in place of the Apple ones (AttentionDescriptor+Parameters.swift). */
+mfa_status_t mfa_attention_kernel_descriptor(const mfa_attention_descriptor_t* desc,
+                                             mfa_kernel_type_t type,
+                                             mfa_kernel_descriptor_t* out);
+
+/* AttentionKernel (AttentionKernel.swift:10-91): the compiled-plan view. `variant` is the
+ * identifier of the HIP kernel instantiation that will run (createSource() has no HIP
+ * meaning; this string replaces it for cache keys and logging). */
+typedef struct mfa_attention_kernel {
+  uint16_t block_parallelization;
+  uint16_t block_traversal;
+  uint16_t block_head;
+  uint16_t threadgroup_size;                /* threads per workgroup (multiple of 64) */
+  uint32_t threadgroup_memory_allocation;   /* LDS bytes per workgroup */
+  float softmax_scale;
+  int32_t type;
+  char variant[96];
+} mfa_attention_kernel_t;
+
+mfa_status_t mfa_attention_kernel_create(const mfa_kernel_descriptor_t* kdesc,
+                                         mfa_attention_kernel_t* out);
+
+/* MultiHeadShape (MultiHeadAttentionDescriptor.swift:11-40). */
+typedef struct mfa_multihead_shape {
+  uint32_t batch_size;
+  uint32_t num_heads;
+  uint32_t sequence_length;
+  uint16_t head_dimension;
+  uint16_t reserved0;
+} mfa_multihead_shape_t;
+
+/* MultiHeadBroadcastMode (MultiHeadAttentionDescriptor.swift:43-109). */
+typedef enum mfa_broadcast_mode {
+  MFA_BROADCAST_STANDARD = 0,
+  MFA_BROADCAST_GROUPED_QUERY = 1,
+  MFA_BROADCAST_MULTI_QUERY = 2,
+  MFA_BROADCAST_CROSS_ATTENTION = 3,
+  MFA_BROADCAST_CUSTOM = 4
+} mfa_broadcast_mode_t;
+
+/* MultiHeadDispatchStrategy (MultiHeadAttentionDescriptor.swift:121-159). All strategies
+ * run the batched 3-D grid here (the reference's perBatchHead binds its slots wrongly,
+ * SURVEY.md §8a quirk 1). */
+typedef enum mfa_dispatch_strategy {
+  MFA_DISPATCH_PER_BATCH_HEAD = 0,
+  MFA_DISPATCH_PER_BATCH = 1,
+  MFA_DISPATCH_BATCHED = 2,
+  MFA_DISPATCH_AUTO = 3
+} mfa_dispatch_strategy_t;
+
+/* MultiHeadAttentionDescriptor (MultiHeadAttentionDescriptor.swift:162-214). */
+typedef struct mfa_multihead_descriptor {
+  mfa_attention_descriptor_t base;
+  mfa_multihead_shape_t query_shape;
+  mfa_multihead_shape_t key_shape;
+  mfa_multihead_shape_t value_shape;
+  int32_t broadcast_mode;     /* mfa_broadcast_mode_t */
+  uint32_t broadcast_param;   /* numKVHeads (groupedQuery) or kvSequenceLength (cross) */
+  int32_t dispatch_strategy;  /* mfa_dispatch_strategy_t */
+} mfa_multihead_descriptor_t;
+
+/* MultiHeadBroadcastMode.isCompatible (MultiHeadAttentionDescriptor.swift:60-107). */
+int mfa_multihead_broadcast_compatible(const mfa_multihead_descriptor_t* desc);
+
+/* Buffers in reference slot order (AttentionOperand.bufferBinding) plus the strides
+ * (slots 5-7 / 10-12 / 9-11) and the mask (slot 12 / 17 / 16).  Strides are HOST arrays
+ * of 4 element strides in BHSD order (setBytes in the reference); NULL = contiguous. */
+typedef struct mfa_attention_buffers {
+  const void* Q;   /* slot 0 */
+  const void* K;   /* slot 1 */
+  const void* V;   /* slot 2 */
+  void* O;         /* slot 3, fp32 dense [B, H, R, D] */
+  void* L;         /* slot 4, [B, H, R]; may be NULL in forward (scratch allocated) */
+  void* D;         /* slot 5, [B, H, R] */
+  const void* dO;  /* slot 6 */
+  void* dV;        /* slot 7, fp32 [B, H_kv, C, D] */
+  void* dK;        /* slot 8, fp32 [B, H_kv, C, D] */
+  void* dQ;        /* slot 9, fp32 [B, H, R, D] */
+  const int64_t* Q_strides;
+  const int64_t* K_strides;
+  const int64_t* V_strides;
+  const void* mask;  /* device pointer; meaning set by base.sparse_mask.mask_type */
+} mfa_attention_buffers_t;
+
+/* MultiHeadAttention.forward / encodeForward (MultiHeadAttention.swift:33-83, :197-234,
+ * dispatchBatched :255-384): grid (ceil(R/Bp), H, B), writes O and L. */
+mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* desc,
+                                   const mfa_attention_buffers_t* buffers, void* stream);
+
+/* MultiHeadAttention.backward (MultiHeadAttention.swift:574-707): backwardQuery (D, dQ)
+ * then backwardKeyValue (dK, dV) on the same stream.  Requires Q K V O L dO D dQ dK dV. */
+mfa_status_t mfa_multihead_backward(const mfa_multihead_descriptor_t* desc,
+                                    const mfa_attention_buffers_t* buffers, void* stream);
+/* The two phases separately (AttentionKernelType.backwardQuery / .backwardKeyValue). */
+mfa_status_t mfa_multihead_backward_query(const mfa_multihead_descriptor_t* desc,
+                                          const mfa_attention_buffers_t* buffers,
+                                          void* stream);
+mfa_status_t mfa_multihead_backward_key_value(const mfa_multihead_descriptor_t* desc,
+                                              const mfa_attention_buffers_t* buffers,
+                                              void* stream);
+
+/* ---------------------------------------------------------------------------------- */
+/* Quantization (Sources/FlashAttention/GEMM/GEMMQuantization.swift).                  */
+
+/* QuantizationMode (GEMMQuantization.swift:27-42). */
+typedef enum mfa_quantization_mode {
+  MFA_QUANT_TENSOR_WISE = 0,
+  MFA_QUANT_BLOCKWISE = 1,
+  MFA_QUANT_ROW_WISE = 2
+} mfa_quantization_mode_t;
+
+/* QuantizationStrategy (GEMMQuantization.swift:45-55). */
+typedef enum mfa_quantization_strategy {
+  MFA_QUANT_STRATEGY_LEGACY = 0,
+  MFA_QUANT_STRATEGY_ASYMMETRIC = 1,
+  MFA_QUANT_STRATEGY_SYMMETRIC = 2
+} mfa_quantization_strategy_t;
+
+/* A QuantizedTensor (GEMMQuantization.swift:681-700) as the kernels consume it.
+ * For FP16/BF16/FP32 precisions the quantization fields are ignored. `data` is a device
+ * pointer to the contiguous [B, H, S, D] tensor (INT4: two values per byte, element 2i in
+ * the low nibble of byte i, GEMMQuantization.swift:500-515).  Blockwise scales are
+ * device arrays indexed (row / bs) * ceil(D / bs) + col / bs over the 2-D view
+ * [B*H*S, D] (GEMMQuantization.swift:561-575). */
+typedef struct mfa_quantized_tensor {
+  const void* data;
+  int32_t precision;           /* mfa_precision_t */
+  float scale;                 /* per-tensor */
+  int32_t zero_point;          /* per-tensor */
+  const float* block_scales;   /* device, NULL unless blockwise */
+  const int32_t* block_zero_points; /* device, NULL unless blockwise */
+  uint32_t block_size;         /* blockSizeK */
+} mfa_quantized_tensor_t;
+
+/* QuantizedAttention.Configuration (QuantizedAttention.swift:12-41). */
+typedef struct mfa_quantized_configuration {
+  int32_t query_precision;  /* default FP16 */
+  int32_t key_precision;    /* default INT8 */
+  int32_t value_precision;  /* default INT8 */
+  int32_t query_strategy, key_strategy, value_strategy;
+  uint8_t strategy_version;
+  uint8_t reserved[3];
+  int32_t mixed_precision_intermediates;
+} mfa_quantized_configuration_t;
+
+void mfa_quantized_configuration_init(mfa_quantized_configuration_t* cfg);
+
+/* QuantizedAttention.QuantizedAttentionDescriptor (QuantizedAttention.swift:58-92) extended
+ * with the multi-head shape the reference expresses through byte offsets. */
+typedef struct mfa_quantized_descriptor {
+  mfa_attention_descriptor_t base;
+  mfa_quantized_configuration_t config;
+  uint32_t batch_size;
+  uint32_t num_heads;
+  uint32_t num_kv_heads;
+  uint32_t reserved0;
+} mfa_quantized_descriptor_t;
+
+/* QuantizedAttention.forward(query:key:value:output:descriptor:...) (:135-263). O fp32,
+ * L base-2 (nullable).  `mask` is the dense fp32 additive mask or NULL. */
+mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* desc,
+                                   const mfa_quantized_tensor_t* query,
+                                   const mfa_quantized_tensor_t* key,
+                                   const mfa_quantized_tensor_t* value, float* output,
+                                   void* logsumexp, const void* mask, void* stream);
+
+/* QuantizedAttention.backwardQuery (:1012-1097) and backwardKeyValue (:1102-1181).
+ * dO/L/D/O use the base descriptor's memory precisions (FP32 unless low precision). */
+mfa_status_t mfa_quantized_backward_query(const mfa_quantized_descriptor_t* desc,
+                                          const mfa_quantized_tensor_t* query,
+                                          const mfa_quantized_tensor_t* key,
+                                          const mfa_quantized_tensor_t* value,
+                                          const float* output, const void* grad_output,
+                                          const void* logsumexp, float* grad_query,
+                                          void* d_values, void* stream);
+mfa_status_t mfa_quantized_backward_key_value(const mfa_quantized_descriptor_t* desc,
+                                              const mfa_quantized_tensor_t* query,
+                                              const mfa_quantized_tensor_t* key,
+                                              const mfa_quantized_tensor_t* value,
+                                              const void* grad_output, const void* logsumexp,
+                                              const void* d_values, float* grad_key,
+                                              float* grad_value, void* stream);
+
+/* GPU runtime quantization (GEMMQuantization.swift:305-623 semantics, bit-exact; the
+ * reference does this on the CPU in QuantizedTensor.from, :720-860).
+ * input: device tensor of `count` elements in `input_precision` (FP32/FP16/BF16), viewed as
+ * 2-D [rows, cols] for blockwise/row-wise.  Writes `output` (INT8 bytes or packed INT4),
+ * and the parameters: `scale_out` (device float[1]) for tensor-wise, `block_scales_out` /
+ * `block_zero_points_out` (device arrays) for blockwise / row-wise.  `workspace` must hold
+ * mfa_quantize_workspace_size() bytes. */
+size_t mfa_quantize_workspace_size(uint64_t count, uint32_t rows, uint32_t cols,
+                                   int32_t mode, uint32_t block_size);
+mfa_status_t mfa_quantize(const void* input, int32_t input_precision, uint64_t count,
+                          uint32_t rows, uint32_t cols, int32_t target_precision,
+                          int32_t mode, uint32_t block_size, void* output, float* scale_out,
+                          float* block_scales_out, int32_t* block_zero_points_out,
+                          void* workspace, void* stream);
+/* Dequantize (GEMMQuantization.swift:529-558 / :629-676) to FP32. */
+mfa_status_t mfa_dequantize(const mfa_quantized_tensor_t* tensor, uint64_t count,
+                            uint32_t cols, float* output, void* stream);
+
+/* ---------------------------------------------------------------------------------- */
+/* GEMM + MLA (Sources/FlashAttention/GEMM/GEMMDescriptor.swift, Attention/            */
+/* MLAOptimizedGEMMMFA.swift).                                                          */
+
+/* GEMMDescriptor (GEMMDescriptor.swift:11-47): C[M,N] = A[M,K] · B[K,N] (+ C when
+ * load_previous_c).  Row-major, leading dimensions default to the packed ones. */
+typedef struct mfa_gemm_descriptor {
+  uint32_t M, N, K;
+  int32_t precision_a, precision_b, precision_c; /* FP16 / BF16 (C may be FP32) */
+  int32_t transpose_a, transpose_b;              /* must be 0 (MLA uses NN) */
+  int32_t load_previous_c;
+  uint32_t lda, ldb, ldc;                        /* 0 = packed */
+  uint32_t batch;                                /* independent GEMMs (grid z) */
+  uint64_t stride_a, stride_b, stride_c;         /* element strides between batch items */
+} mfa_gemm_descriptor_t;
+
+mfa_status_t mfa_gemm(const mfa_gemm_descriptor_t* desc, const void* A, const void* B,
+                      void* C, void* stream);
+
+/* MLAOptimizedGEMMMFA.forward (MLAOptimizedGEMMMFA.swift:158-240) followed by the
+ * attention forward the reference's caller runs on the decompressed BSHD K/V
+ * (KernelRegressionTests.swift:398-465 stride pattern).
+ *   kv_latent [B*S_kv, latent_dim], w_k / w_v [latent_dim, H*D] (precision FP16/BF16),
+ *   query BHSD [B, H, S_q, D] in the same precision, K/V scratch [B*S_kv, H*D] (caller
+ *   provided or NULL → library-owned), output fp32 [B, H, S_q, D], L nullable. */
+typedef struct mfa_mla_descriptor {
+  mfa_attention_descriptor_t base; /* precision / sparsity / scale of the attention */
+  uint32_t batch_size;
+  uint32_t num_heads;
+  uint32_t sequence_length_q;
+  uint32_t sequence_length_kv;
+  uint32_t head_dim;
+  uint32_t kv_latent_dim;
+  int32_t precision;                /* FP16 or BF16 for latent / weights / Q / K / V */
+} mfa_mla_descriptor_t;
+
+mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const void* kv_latent,
+                             const void* w_k, const void* w_v, const void* query,
+                             void* decompressed_k, void* decompressed_v, float* output,
+                             void* logsumexp, void* stream);
+
+/* ---------------------------------------------------------------------------------- */
+/* Host utilities mirrored from the reference.                                          */
+
+/* MaskingStrategyHeuristic.sequenceBucket / defaultRule (MaskingStrategyHeuristic.swift:
+ * 47-60, :111-136).  Returns 0 = elementWise, 1 = bitmask.  The two strategies are
+ * numerically identical; on gfx950 the predicate is evaluated per element either way. */
+int mfa_masking_sequence_bucket(int sequence_length);
+int mfa_masking_default_rule(int sequence_length, int head_dimension);
+
+/* SparseMQABuilder (Attention/SparseMQABuilder.swift:4-62), host arrays of uint32 pairs. */
+void mfa_sparse_build_sliding_window(uint32_t sequence_length, uint32_t window_size,
+                                     uint32_t* ranges_out);
+void mfa_sparse_build_block_sparse(const uint8_t* pattern, uint32_t rows, uint32_t cols,
+                                   uint32_t block_size, uint32_t* ranges_out);
+
+/* Version / error / device utilities. */
+const char* mfa_version(void);
+const char* mfa_last_error(void);
+int mfa_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MFA_MFA_H */

@@ -1,0 +1,789 @@
+// mfa_api.cpp — host layer behind include/mfa/mfa.h.
+//
+// This replaces the reference's Swift host code: descriptor -> kernel plan
+// (AttentionDescriptor.kernelDescriptor, AttentionKernel.init), buffer-slot binding and grid
+// sizing (MultiHeadAttention.dispatchBatched / backward, QuantizedAttention.forward /
+// backwardQuery / backwardKeyValue, MLAOptimizedGEMMMFA.forward).  Instead of generating and
+// JIT-compiling Metal source per shape, every configuration maps onto one of a fixed set of
+// precompiled gfx950 kernel instantiations (see mfa_dispatch.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/mfa/mfa.h"
+#include "mfa_dispatch.h"
+#include "mfa_params.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+mfa_status_t fail(mfa_status_t code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  if (getenv("MFA_DEBUG")) fprintf(stderr, "[mfa] %s\n", buf);
+  return code;
+}
+
+mfa_status_t hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return MFA_SUCCESS;
+  return fail(MFA_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+}
+
+int precision_size(int p) {
+  switch (p) {
+    case MFA_PRECISION_FP32: return 4;
+    case MFA_PRECISION_FP16:
+    case MFA_PRECISION_BF16: return 2;
+    default: return 1;
+  }
+}
+
+bool is_quantized(int p) { return p == MFA_PRECISION_INT8 || p == MFA_PRECISION_INT4; }
+
+int pad_head(int D) {
+  if (D <= 32) return 32;
+  if (D <= 64) return 64;
+  if (D <= 128) return 128;
+  if (D <= 256) return 256;
+  return -1;
+}
+
+// Library-owned scratch (L when the caller passes none: MultiHeadAttention.swift:296-319
+// allocates and zero-fills one per call).  One buffer per device, grown on demand.
+struct Scratch {
+  std::mutex mu;
+  void* ptr[64] = {};
+  size_t bytes[64] = {};
+} g_scratch;
+
+mfa_status_t scratch(size_t bytes, void** out, int slot_hint = 0) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(MFA_ERR_NO_DEVICE, "no HIP device");
+  const int slot = (dev * 4 + slot_hint) % 64;
+  std::lock_guard<std::mutex> lock(g_scratch.mu);
+  if (g_scratch.bytes[slot] < bytes) {
+    if (g_scratch.ptr[slot]) (void)hipFree(g_scratch.ptr[slot]);
+    g_scratch.ptr[slot] = nullptr;
+    g_scratch.bytes[slot] = 0;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return hip_status(e, "hipMalloc(scratch)");
+    g_scratch.ptr[slot] = p;
+    g_scratch.bytes[slot] = bytes;
+  }
+  *out = g_scratch.ptr[slot];
+  return MFA_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------------------
+// Precision policy (AttentionDescriptor+Precisions.swift:12-242), gfx950 register column.
+struct Precisions {
+  int mem[MFA_OPERAND_COUNT];
+  int reg[MFA_OPERAND_COUNT];
+};
+
+Precisions resolve_precisions(const mfa_attention_descriptor_t& d) {
+  Precisions p;
+  for (int i = 0; i < MFA_OPERAND_COUNT; ++i) p.mem[i] = p.reg[i] = -1;
+  const int input = d.input_memory_precision == MFA_PRECISION_UNSET ? MFA_PRECISION_FP16
+                                                                     : d.input_memory_precision;
+  const int in_mem = d.low_precision_inputs ? input : MFA_PRECISION_FP32;
+  p.mem[MFA_OPERAND_Q] = p.mem[MFA_OPERAND_K] = p.mem[MFA_OPERAND_V] = in_mem;
+  p.mem[MFA_OPERAND_dO] = in_mem;
+  p.mem[MFA_OPERAND_L] = d.low_precision_intermediates ? MFA_PRECISION_FP16 : MFA_PRECISION_FP32;
+  p.mem[MFA_OPERAND_D] = d.low_precision_intermediates ? MFA_PRECISION_BF16 : MFA_PRECISION_FP32;
+  p.mem[MFA_OPERAND_O] = p.mem[MFA_OPERAND_dV] = p.mem[MFA_OPERAND_dK] = p.mem[MFA_OPERAND_dQ] =
+      MFA_PRECISION_FP32;
+  // Registers as the gfx950 kernels hold them: MFMA operands in the input type, every
+  // accumulator (S, dP, O, dV, dK, dQ) FP32, P and dS rounded to the MFMA operand type.
+  const int in_reg = in_mem;
+  p.reg[MFA_OPERAND_Q] = p.reg[MFA_OPERAND_K] = p.reg[MFA_OPERAND_V] = in_reg;
+  p.reg[MFA_OPERAND_dO] = in_reg;
+  p.reg[MFA_OPERAND_L] = p.reg[MFA_OPERAND_D] = MFA_PRECISION_FP32;
+  p.reg[MFA_OPERAND_S] = p.reg[MFA_OPERAND_dP] = MFA_PRECISION_FP32;
+  p.reg[MFA_OPERAND_P] = p.reg[MFA_OPERAND_dS] = in_reg;
+  p.reg[MFA_OPERAND_O] = p.reg[MFA_OPERAND_dV] = p.reg[MFA_OPERAND_dK] =
+      p.reg[MFA_OPERAND_dQ] = MFA_PRECISION_FP32;
+  return p;
+}
+
+int elem_of(int prec) {
+  switch (prec) {
+    case MFA_PRECISION_FP32: return 0;
+    case MFA_PRECISION_FP16: return 1;
+    case MFA_PRECISION_BF16: return 2;
+    default: return -1;
+  }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+mfa::Operand make_operand(const void* ptr, int prec, int B, int Hx, int S, int D,
+                          const int64_t* strides, int transposed) {
+  mfa::Operand op;
+  memset(&op, 0, sizeof(op));
+  op.ptr = ptr;
+  op.prec = prec;
+  if (strides) {
+    op.sb = strides[0]; op.sh = strides[1]; op.ss = strides[2]; op.sd = strides[3];
+  } else if (transposed) {
+    // Column-major within a head: element (s, d) at d * S + s
+    // (AttentionKernelDescriptor.transposeState, AttentionKernelDescriptor.swift:34-47).
+    op.sd = S; op.ss = 1; op.sh = (int64_t)S * D; op.sb = (int64_t)Hx * S * D;
+  } else {
+    op.sd = 1; op.ss = D; op.sh = (int64_t)S * D; op.sb = (int64_t)Hx * S * D;
+  }
+  const int es = precision_size(prec);
+  const int vbytes = prec == MFA_PRECISION_INT8 ? 8 : 16;
+  op.vec = (op.sd == 1) && ((uintptr_t)ptr % vbytes == 0) && ((op.ss * es) % vbytes == 0) &&
+           ((op.sh * es) % vbytes == 0) && ((op.sb * es) % vbytes == 0) &&
+           prec != MFA_PRECISION_INT4;
+  op.scale = 1.f;
+  op.zp = 0;
+  op.cols = D;
+  (void)B;
+  return op;
+}
+
+struct MaskPlan {
+  mfa::MaskArgs args;
+};
+
+mfa_status_t plan_masks(const mfa_attention_descriptor_t& base, const void* mask, int R, int C,
+                        mfa::MaskArgs* out) {
+  memset(out, 0, sizeof(*out));
+  switch (base.sparsity_pattern) {
+    case MFA_SPARSITY_NONE:
+    case MFA_SPARSITY_CUSTOM:  // treated as none (AttentionDescriptor.swift:226-229)
+      break;
+    case MFA_SPARSITY_CAUSAL: out->causal = 1; break;
+    case MFA_SPARSITY_SLIDING_WINDOW:
+      out->window = 1;
+      out->window_size = base.window_size;
+      break;
+    default: return fail(MFA_ERR_INVALID_DESCRIPTOR, "unknown sparsity pattern %d",
+                         base.sparsity_pattern);
+  }
+  if (base.has_sparse_mask) {
+    switch (base.mask_type) {
+      case MFA_MASK_DENSE: out->amask = (const float*)mask; break;
+      case MFA_MASK_SPARSE_RANGES: out->ranges = (const uint32_t*)mask; break;
+      case MFA_MASK_BLOCK_SPARSE:
+        // HAS_BLOCK_SPARSE only enables the mask block; no predicate reads the buffer
+        // and the external additive mask is skipped (AttentionKernel+Softmax.swift:306, :371).
+        break;
+      default: return fail(MFA_ERR_INVALID_DESCRIPTOR, "unknown mask type %d", base.mask_type);
+    }
+  } else {
+    out->amask = (const float*)mask;  // forward(maskBuffer:) dense additive mask
+  }
+  // Fully masked tiles may be skipped only when no row is masked everywhere (otherwise the
+  // reference's finite mask value makes such a row a uniform average over every key).
+  const bool rows_safe = !out->ranges && (!out->window || (int64_t)R <= (int64_t)C + out->window_size);
+  out->skip_ok = rows_safe ? 1 : 0;
+  return MFA_SUCCESS;
+}
+
+float resolve_scale(const mfa_attention_descriptor_t& d, int head_dim) {
+  // AttentionKernel.swift:63-68: default 1/sqrt(head_dim).
+  if (d.has_softmax_scale) return d.softmax_scale;
+  return 1.0f / std::sqrt((float)head_dim);
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+const char* mfa_version(void) { return "mfa-cdna4 0.1.0 (gfx950)"; }
+const char* mfa_last_error(void) { return g_last_error.c_str(); }
+int mfa_abi_version(void) { return MFA_ABI_VERSION; }
+
+int mfa_operand_buffer_binding(mfa_operand_t operand) {
+  switch (operand) {
+    case MFA_OPERAND_Q: return 0;
+    case MFA_OPERAND_K: return 1;
+    case MFA_OPERAND_V: return 2;
+    case MFA_OPERAND_O: return 3;
+    case MFA_OPERAND_L: return 4;
+    case MFA_OPERAND_D: return 5;
+    case MFA_OPERAND_dO: return 6;
+    case MFA_OPERAND_dV: return 7;
+    case MFA_OPERAND_dK: return 8;
+    case MFA_OPERAND_dQ: return 9;
+    default: return -1;
+  }
+}
+
+void mfa_attention_descriptor_init(mfa_attention_descriptor_t* d) {
+  memset(d, 0, sizeof(*d));
+  d->input_memory_precision = MFA_PRECISION_UNSET;
+  d->sparsity_pattern = MFA_SPARSITY_NONE;
+  d->mask_type = MFA_MASK_DENSE;
+  d->num_kv_heads = 1;
+}
+
+void mfa_quantized_configuration_init(mfa_quantized_configuration_t* c) {
+  memset(c, 0, sizeof(*c));
+  c->query_precision = MFA_PRECISION_FP16;
+  c->key_precision = MFA_PRECISION_INT8;
+  c->value_precision = MFA_PRECISION_INT8;
+  c->strategy_version = 1;  // QuantizationStrategy.currentVersion
+  c->mixed_precision_intermediates = 1;
+}
+
+mfa_status_t mfa_attention_kernel_descriptor(const mfa_attention_descriptor_t* desc,
+                                             mfa_kernel_type_t type,
+                                             mfa_kernel_descriptor_t* out) {
+  if (!desc || !out) return fail(MFA_ERR_INVALID_ARGUMENT, "null descriptor");
+  if (!desc->has_matrix_dimensions || !desc->has_transpose_state)
+    return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
+  memset(out, 0, sizeof(*out));
+  const Precisions pr = resolve_precisions(*desc);
+  const int D = desc->head;
+  const int DP = pad_head(D);
+  if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", D);
+  const int elem = elem_of(pr.mem[MFA_OPERAND_Q]);
+  if (elem < 0) return fail(MFA_ERR_UNSUPPORTED, "input precision");
+  int bp = 0, bt = 0, nw = 0;
+  if (type == MFA_KERNEL_FORWARD || type == MFA_KERNEL_MLA_COMPRESSED)
+    mfa::fwd_block_config(elem, DP, &bp, &bt, &nw);
+  else
+    mfa::bwd_block_config(elem, DP, &bp, &bt, &nw);
+  out->block_parallelization = (uint16_t)bp;
+  out->block_traversal = (uint16_t)bt;
+  // Head block = whole padded head (accumulators stay in registers), clamped to the padded
+  // head dimension as AttentionDescriptor.swift:90-105 does.
+  out->block_head = (uint16_t)std::min(DP, (D + 7) / 8 * 8);
+  out->head_dimension = (uint16_t)D;
+  out->sequence_length = std::max(desc->row, desc->column);
+  for (int i = 0; i < MFA_OPERAND_COUNT; ++i) {
+    out->memory_precisions[i] = pr.mem[i];
+    out->register_precisions[i] = pr.reg[i];
+    out->cache_state[i] = 0;
+    out->transpose_state[i] = 0;
+  }
+  switch (type) {
+    case MFA_KERNEL_FORWARD:
+    case MFA_KERNEL_MLA_COMPRESSED:
+      out->cache_state[MFA_OPERAND_Q] = out->cache_state[MFA_OPERAND_O] = 1;
+      break;
+    case MFA_KERNEL_BACKWARD_QUERY:
+      out->cache_state[MFA_OPERAND_Q] = out->cache_state[MFA_OPERAND_dO] =
+          out->cache_state[MFA_OPERAND_dQ] = 1;
+      break;
+    case MFA_KERNEL_BACKWARD_KEY_VALUE:
+      out->cache_state[MFA_OPERAND_K] = out->cache_state[MFA_OPERAND_V] =
+          out->cache_state[MFA_OPERAND_dK] = out->cache_state[MFA_OPERAND_dV] = 1;
+      break;
+  }
+  out->transpose_state[MFA_OPERAND_Q] = out->transpose_state[MFA_OPERAND_dQ] = desc->transpose_q;
+  out->transpose_state[MFA_OPERAND_K] = out->transpose_state[MFA_OPERAND_dK] = desc->transpose_k;
+  out->transpose_state[MFA_OPERAND_V] = out->transpose_state[MFA_OPERAND_dV] = desc->transpose_v;
+  out->transpose_state[MFA_OPERAND_O] = out->transpose_state[MFA_OPERAND_dO] = desc->transpose_o;
+  // gfx950 stages every tile through LDS with register prefetch.
+  out->prefer_async_cache = 1;
+  out->prefer_async_load = 0;
+  out->has_softmax_scale = desc->has_softmax_scale;
+  out->softmax_scale = desc->softmax_scale;
+  out->type = type;
+  out->masking_strategy_override = -1;
+  return MFA_SUCCESS;
+}
+
+mfa_status_t mfa_attention_kernel_create(const mfa_kernel_descriptor_t* k,
+                                         mfa_attention_kernel_t* out) {
+  if (!k || !out) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  if (k->block_parallelization == 0 || k->head_dimension == 0)
+    return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
+  memset(out, 0, sizeof(*out));
+  const int DP = pad_head(k->head_dimension);
+  if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension > 256");
+  const int elem = elem_of(k->memory_precisions[MFA_OPERAND_Q]);
+  if (elem < 0) return fail(MFA_ERR_UNSUPPORTED, "input precision");
+  out->block_parallelization = k->block_parallelization;
+  out->block_traversal = k->block_traversal;
+  out->block_head = k->block_head;
+  out->threadgroup_size = (uint16_t)(k->block_parallelization / 32 * 64);
+  out->softmax_scale = k->has_softmax_scale ? k->softmax_scale
+                                            : 1.0f / std::sqrt((float)k->head_dimension);
+  out->type = k->type;
+  const char* en = elem == 0 ? "f32" : elem == 1 ? "f16" : "bf16";
+  switch (k->type) {
+    case MFA_KERNEL_FORWARD:
+    case MFA_KERNEL_MLA_COMPRESSED:
+      out->threadgroup_memory_allocation = (uint32_t)mfa::fwd_lds_bytes(elem, DP);
+      snprintf(out->variant, sizeof(out->variant), "mfa_fwd_%s_d%d_bq%d_bk%d", en, DP,
+               k->block_parallelization, k->block_traversal);
+      break;
+    case MFA_KERNEL_BACKWARD_QUERY:
+      out->threadgroup_memory_allocation = (uint32_t)mfa::bwd_lds_bytes(0, elem, DP);
+      snprintf(out->variant, sizeof(out->variant), "mfa_bwd_q_%s_d%d_bq%d_bk%d", en, DP,
+               k->block_parallelization, k->block_traversal);
+      break;
+    case MFA_KERNEL_BACKWARD_KEY_VALUE:
+      out->threadgroup_memory_allocation = (uint32_t)mfa::bwd_lds_bytes(1, elem, DP);
+      snprintf(out->variant, sizeof(out->variant), "mfa_bwd_kv_%s_d%d_bk%d_bq%d", en, DP,
+               k->block_parallelization, k->block_traversal);
+      break;
+  }
+  return MFA_SUCCESS;
+}
+
+int mfa_multihead_broadcast_compatible(const mfa_multihead_descriptor_t* d) {
+  const mfa_multihead_shape_t& q = d->query_shape;
+  const mfa_multihead_shape_t& k = d->key_shape;
+  const mfa_multihead_shape_t& v = d->value_shape;
+  const bool same_b = q.batch_size == k.batch_size && k.batch_size == v.batch_size;
+  const bool same_d = q.head_dimension == k.head_dimension && k.head_dimension == v.head_dimension;
+  switch (d->broadcast_mode) {
+    case MFA_BROADCAST_STANDARD:
+      return same_b && q.num_heads == k.num_heads && k.num_heads == v.num_heads && same_d &&
+             k.sequence_length == v.sequence_length;
+    case MFA_BROADCAST_GROUPED_QUERY: {
+      const uint32_t n = d->broadcast_param;
+      return same_b && n > 0 && k.num_heads == n && v.num_heads == n && q.num_heads % n == 0 &&
+             same_d && k.sequence_length == v.sequence_length;
+    }
+    case MFA_BROADCAST_MULTI_QUERY:
+      return same_b && k.num_heads == 1 && v.num_heads == 1 && same_d &&
+             k.sequence_length == v.sequence_length;
+    case MFA_BROADCAST_CROSS_ATTENTION: {
+      const uint32_t s = d->broadcast_param;
+      return same_b && q.num_heads == k.num_heads && k.num_heads == v.num_heads && same_d &&
+             k.sequence_length == s && v.sequence_length == s;
+    }
+    case MFA_BROADCAST_CUSTOM:
+      return 1;  // explicit shapes are taken as given
+    default:
+      return 0;
+  }
+}
+
+}  // extern "C"
+
+// =========================================================================================
+// Forward.
+namespace {
+
+struct MHAPlan {
+  int B, H, Hkv, R, C, D, DP, elem;
+  float scale;
+  Precisions pr;
+  mfa::MaskArgs mask;
+};
+
+mfa_status_t plan_multihead(const mfa_multihead_descriptor_t* desc, const void* mask,
+                            MHAPlan* pl) {
+  if (!desc) return fail(MFA_ERR_INVALID_ARGUMENT, "null descriptor");
+  if (!mfa_multihead_broadcast_compatible(desc))
+    return fail(MFA_ERR_INVALID_DESCRIPTOR, "Incompatible tensor shapes for broadcast mode %d",
+                desc->broadcast_mode);
+  const mfa_attention_descriptor_t& base = desc->base;
+  if (!base.has_transpose_state) return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
+  pl->B = (int)desc->query_shape.batch_size;
+  pl->H = (int)desc->query_shape.num_heads;
+  pl->Hkv = (int)desc->key_shape.num_heads;
+  pl->R = (int)desc->query_shape.sequence_length;
+  pl->C = (int)desc->key_shape.sequence_length;
+  pl->D = (int)desc->query_shape.head_dimension;
+  if (pl->B <= 0 || pl->H <= 0 || pl->Hkv <= 0 || pl->D <= 0)
+    return fail(MFA_ERR_INVALID_DESCRIPTOR, "empty shape");
+  pl->DP = pad_head(pl->D);
+  if (pl->DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", pl->D);
+  pl->pr = resolve_precisions(base);
+  pl->elem = elem_of(pl->pr.mem[MFA_OPERAND_Q]);
+  if (pl->elem < 0) return fail(MFA_ERR_UNSUPPORTED, "input precision %d", pl->pr.mem[MFA_OPERAND_Q]);
+  pl->scale = resolve_scale(base, pl->D);
+  return plan_masks(base, mask, pl->R, pl->C, &pl->mask);
+}
+
+}  // namespace
+
+extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* desc,
+                                              const mfa_attention_buffers_t* buf,
+                                              void* stream) {
+  if (!buf || !buf->Q || !buf->K || !buf->V || !buf->O)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "forward requires Q, K, V, O");
+  MHAPlan pl;
+  mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
+  if (st != MFA_SUCCESS) return st;
+  if (pl.R == 0) return MFA_SUCCESS;
+  const mfa_attention_descriptor_t& base = desc->base;
+  const int prec = pl.pr.mem[MFA_OPERAND_Q];
+
+  mfa::FwdParams p;
+  memset(&p, 0, sizeof(p));
+  p.q = make_operand(buf->Q, prec, pl.B, pl.H, pl.R, pl.D, buf->Q_strides, base.transpose_q);
+  p.k = make_operand(buf->K, prec, pl.B, pl.Hkv, pl.C, pl.D, buf->K_strides, base.transpose_k);
+  p.v = make_operand(buf->V, prec, pl.B, pl.Hkv, pl.C, pl.D, buf->V_strides, base.transpose_v);
+  p.o = (float*)buf->O;
+  p.o_ss = pl.D;
+  p.o_sh = (int64_t)pl.R * pl.D;
+  p.o_sb = (int64_t)pl.H * pl.R * pl.D;
+  p.l_f16 = pl.pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+  void* L = buf->L;
+  if (!L) {
+    st = scratch((size_t)pl.B * pl.H * pl.R * 4, &L, 0);
+    if (st != MFA_SUCCESS) return st;
+  }
+  p.l = L;
+  p.B = pl.B; p.H = pl.H; p.Hkv = pl.Hkv; p.R = pl.R; p.C = pl.C; p.D = pl.D;
+  int bq, bk, nw;
+  mfa::fwd_block_config(pl.elem, pl.DP, &bq, &bk, &nw);
+  p.nblk = (pl.R + bq - 1) / bq;
+  p.c_log2 = 1.442695041f * pl.scale;  // dotProductScale (AttentionKernel+Softmax.swift:17-25)
+  p.o_mul = 1.f;
+  p.mask = pl.mask;
+  return hip_status(mfa::fwd_dispatch(p, pl.elem, pl.DP, 0, 0, (hipStream_t)stream),
+                    "mfa_fwd launch");
+}
+
+// =========================================================================================
+// Quantized forward (QuantizedAttention.forward, QuantizedAttention.swift:135-263).
+namespace {
+
+int src_kind(int prec) {
+  if (prec == MFA_PRECISION_INT8) return 1;
+  if (prec == MFA_PRECISION_INT4) return 2;
+  return 0;
+}
+
+mfa_status_t quant_operand(const mfa_quantized_tensor_t* t, int cfg_prec, int B, int Hx, int S,
+                           int D, mfa::Operand* op, float* fold) {
+  if (!t || !t->data) return fail(MFA_ERR_INVALID_ARGUMENT, "null quantized tensor");
+  const int prec = cfg_prec;
+  *op = make_operand(t->data, prec, B, Hx, S, D, nullptr, 0);
+  *fold = 1.f;
+  if (is_quantized(prec)) {
+    if (t->block_scales) {
+      if (t->block_size == 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "blockwise tensor with block size 0");
+      op->bscale = t->block_scales;
+      op->bzp = t->block_zero_points;
+      op->bsize = (int)t->block_size;
+      op->bcols = (D + (int)t->block_size - 1) / (int)t->block_size;
+    } else {
+      *fold = t->scale;
+      op->zp = t->zero_point;
+      // (q - zp) must stay exact in the 16-bit MFMA operand.
+      if (t->zero_point < -128 || t->zero_point > 128)
+        return fail(MFA_ERR_UNSUPPORTED, "zero point %d outside [-128, 128]", t->zero_point);
+    }
+  }
+  return MFA_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* desc,
+                                              const mfa_quantized_tensor_t* query,
+                                              const mfa_quantized_tensor_t* key,
+                                              const mfa_quantized_tensor_t* value, float* output,
+                                              void* logsumexp, const void* mask, void* stream) {
+  if (!desc || !output) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  const mfa_attention_descriptor_t& base = desc->base;
+  if (!base.has_matrix_dimensions) return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
+  const int B = desc->batch_size ? (int)desc->batch_size : 1;
+  const int H = desc->num_heads ? (int)desc->num_heads : 1;
+  const int Hkv = desc->num_kv_heads ? (int)desc->num_kv_heads : H;
+  const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
+  const int DP = pad_head(D);
+  if (DP < 0 || D <= 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d", D);
+  const mfa_quantized_configuration_t& cfg = desc->config;
+  const int qp = cfg.query_precision, kp = cfg.key_precision, vp = cfg.value_precision;
+  // Compute element type: the floating-point input type, FP16 when every input is integer.
+  int elem = -1;
+  for (int p : {qp, kp, vp}) {
+    if (!is_quantized(p)) {
+      const int e = elem_of(p);
+      if (elem >= 0 && e != elem) return fail(MFA_ERR_UNSUPPORTED, "mixed floating-point input precisions");
+      elem = e;
+    }
+  }
+  if (elem < 0) elem = 1;
+  if (src_kind(kp) != src_kind(vp))
+    return fail(MFA_ERR_UNSUPPORTED, "K and V must share a precision class");
+  if (elem == 0 && (is_quantized(qp) || is_quantized(kp)))
+    return fail(MFA_ERR_UNSUPPORTED, "FP32 query with quantized K/V");
+
+  mfa::FwdParams p;
+  memset(&p, 0, sizeof(p));
+  float fq = 1.f, fk = 1.f, fv = 1.f;
+  mfa_status_t st;
+  if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv)) != MFA_SUCCESS) return st;
+  p.o = output;
+  p.o_ss = D; p.o_sh = (int64_t)R * D; p.o_sb = (int64_t)H * R * D;
+  const Precisions pr = resolve_precisions(base);
+  p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+  void* L = logsumexp;
+  if (!L) {
+    if ((st = scratch((size_t)B * H * R * 4, &L, 0)) != MFA_SUCCESS) return st;
+  }
+  p.l = L;
+  p.B = B; p.H = H; p.Hkv = Hkv; p.R = R; p.C = C; p.D = D;
+  int bq, bk, nw;
+  mfa::fwd_block_config(elem, DP, &bq, &bk, &nw);
+  p.nblk = (R + bq - 1) / bq;
+  const float scale = resolve_scale(base, D);
+  p.c_log2 = 1.442695041f * scale * fq * fk;
+  p.o_mul = fv;
+  if ((st = plan_masks(base, mask, R, C, &p.mask)) != MFA_SUCCESS) return st;
+  if (R == 0) return MFA_SUCCESS;
+  return hip_status(mfa::fwd_dispatch(p, elem, DP, src_kind(kp), src_kind(vp), (hipStream_t)stream),
+                    "mfa_fwd (quantized) launch");
+}
+
+// =========================================================================================
+// Host utilities.
+extern "C" int mfa_masking_sequence_bucket(int sequence_length) {
+  // MaskingStrategyHeuristic.sequenceBucket (MaskingStrategyHeuristic.swift:47-60).
+  static const int anchors[] = {64, 128, 256, 512, 768, 1024, 1536, 2048, 3072, 4096};
+  int best = anchors[0];
+  int best_delta = std::abs(sequence_length - best);
+  for (int i = 1; i < 10; ++i) {
+    const int delta = std::abs(sequence_length - anchors[i]);
+    if (delta < best_delta) {
+      best = anchors[i];
+      best_delta = delta;
+    }
+  }
+  return best;
+}
+
+extern "C" int mfa_masking_default_rule(int s, int h) {
+  // MaskingStrategyHeuristic.defaultRule (MaskingStrategyHeuristic.swift:111-136);
+  // 1 = bitmask, 0 = elementWise.
+  if (h == 192) return 1;
+  if (s >= 4096) return 0;
+  if (s >= 1792 && s <= 2560) return 1;
+  if (h == 128) return s <= 256 ? 1 : 0;
+  if (s <= 256) return 1;
+  if (h == 256 && s >= 1024) return 0;
+  return 1;
+}
+
+extern "C" void mfa_sparse_build_sliding_window(uint32_t n, uint32_t window, uint32_t* out) {
+  // SparseMQABuilder.buildSlidingWindow (SparseMQABuilder.swift:4-28).
+  const int64_t capped = std::max<int64_t>(1, (int64_t)window);
+  const int64_t half = capped / 2;
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    out[2 * i] = (uint32_t)std::max<int64_t>(0, i - half);
+    out[2 * i + 1] = (uint32_t)std::min<int64_t>((int64_t)n, i + half);
+  }
+}
+
+extern "C" void mfa_sparse_build_block_sparse(const uint8_t* pattern, uint32_t rows,
+                                              uint32_t cols, uint32_t block_size,
+                                              uint32_t* out) {
+  // SparseMQABuilder.buildBlockSparse (SparseMQABuilder.swift:30-62).
+  for (uint32_t r = 0; r < rows; ++r) {
+    int64_t first = -1, last = -1;
+    for (uint32_t c = 0; c < cols; ++c)
+      if (pattern[(size_t)r * cols + c]) {
+        if (first < 0) first = c;
+        last = c;
+      }
+    if (first >= 0) {
+      const int64_t maxc = (int64_t)cols * block_size;
+      out[2 * r] = (uint32_t)(first * block_size);
+      out[2 * r + 1] = (uint32_t)std::min<int64_t>((last + 1) * block_size, maxc);
+    } else {
+      out[2 * r] = 0;
+      out[2 * r + 1] = 0;
+    }
+  }
+}
+
+// =========================================================================================
+// Backward (MultiHeadAttention.backward, MultiHeadAttention.swift:574-707).
+namespace {
+
+enum BwdPhase { PHASE_QUERY = 1, PHASE_KV = 2, PHASE_BOTH = 3 };
+
+mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ksrc, int qsrc,
+                          int phase, hipStream_t stream) {
+  mfa::BwdParams p = base_p;
+  int bp, bt, nw;
+  mfa::bwd_block_config(elem, DP, &bp, &bt, &nw);
+  if (phase & PHASE_QUERY) {
+    p.nblk = (p.R + bp - 1) / bp;
+    if (p.R > 0) {
+      mfa_status_t st = hip_status(mfa::bwd_q_dispatch(p, elem, DP, ksrc, ksrc, stream),
+                                   "mfa_bwd_q launch");
+      if (st != MFA_SUCCESS) return st;
+    }
+  }
+  if (phase & PHASE_KV) {
+    p.nblk = (p.C + bp - 1) / bp;
+    if (p.C > 0) {
+      mfa_status_t st = hip_status(mfa::bwd_kv_dispatch(p, elem, DP, ksrc, qsrc, stream),
+                                   "mfa_bwd_kv launch");
+      if (st != MFA_SUCCESS) return st;
+    }
+  }
+  return MFA_SUCCESS;
+}
+
+mfa_status_t multihead_backward(const mfa_multihead_descriptor_t* desc,
+                                const mfa_attention_buffers_t* buf, void* stream, int phase) {
+  if (!buf) return fail(MFA_ERR_INVALID_ARGUMENT, "null buffers");
+  const bool need_q = phase & PHASE_QUERY, need_kv = phase & PHASE_KV;
+  if (!buf->Q || !buf->K || !buf->V || !buf->L || !buf->D || !buf->dO ||
+      (need_q && (!buf->O || !buf->dQ)) || (need_kv && (!buf->dK || !buf->dV)))
+    return fail(MFA_ERR_INVALID_ARGUMENT, "backward requires Q K V O L D dO and the gradients");
+  MHAPlan pl;
+  mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
+  if (st != MFA_SUCCESS) return st;
+  const mfa_attention_descriptor_t& base = desc->base;
+  const int prec = pl.pr.mem[MFA_OPERAND_Q];
+  mfa::BwdParams p;
+  memset(&p, 0, sizeof(p));
+  p.q = make_operand(buf->Q, prec, pl.B, pl.H, pl.R, pl.D, buf->Q_strides, base.transpose_q);
+  p.k = make_operand(buf->K, prec, pl.B, pl.Hkv, pl.C, pl.D, buf->K_strides, base.transpose_k);
+  p.v = make_operand(buf->V, prec, pl.B, pl.Hkv, pl.C, pl.D, buf->V_strides, base.transpose_v);
+  p.dO_op = make_operand(buf->dO, pl.pr.mem[MFA_OPERAND_dO], pl.B, pl.H, pl.R, pl.D, nullptr,
+                         base.transpose_o);
+  p.o = (const float*)buf->O;
+  p.l = buf->L;
+  p.l_f16 = pl.pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+  p.dD = buf->D;
+  p.d_bf16 = pl.pr.mem[MFA_OPERAND_D] == MFA_PRECISION_BF16;
+  p.dq = (float*)buf->dQ;
+  p.dk = (float*)buf->dK;
+  p.dv = (float*)buf->dV;
+  p.B = pl.B; p.H = pl.H; p.Hkv = pl.Hkv; p.R = pl.R; p.C = pl.C; p.D = pl.D;
+  p.group = pl.H / pl.Hkv;
+  p.c_log2 = 1.442695041f * pl.scale;
+  p.scale = pl.scale;
+  p.dscale = pl.scale;
+  p.dq_mul = 1.f;
+  p.dk_mul = 1.f;
+  p.mask = pl.mask;
+  return run_backward(p, pl.elem, pl.DP, 0, 0, phase, (hipStream_t)stream);
+}
+
+}  // namespace
+
+extern "C" mfa_status_t mfa_multihead_backward(const mfa_multihead_descriptor_t* desc,
+                                               const mfa_attention_buffers_t* buffers,
+                                               void* stream) {
+  return multihead_backward(desc, buffers, stream, PHASE_BOTH);
+}
+extern "C" mfa_status_t mfa_multihead_backward_query(const mfa_multihead_descriptor_t* desc,
+                                                     const mfa_attention_buffers_t* buffers,
+                                                     void* stream) {
+  return multihead_backward(desc, buffers, stream, PHASE_QUERY);
+}
+extern "C" mfa_status_t mfa_multihead_backward_key_value(const mfa_multihead_descriptor_t* desc,
+                                                         const mfa_attention_buffers_t* buffers,
+                                                         void* stream) {
+  return multihead_backward(desc, buffers, stream, PHASE_KV);
+}
+
+// Quantized backward (QuantizedAttention.backwardQuery / backwardKeyValue,
+// QuantizedAttention.swift:1012-1181).
+namespace {
+
+mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
+                                const mfa_quantized_tensor_t* query,
+                                const mfa_quantized_tensor_t* key,
+                                const mfa_quantized_tensor_t* value, const float* output,
+                                const void* grad_output, const void* logsumexp,
+                                float* grad_query, float* grad_key, float* grad_value,
+                                void* d_values, int phase, void* stream) {
+  if (!desc || !grad_output || !logsumexp || !d_values)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  if ((phase & PHASE_QUERY) && (!output || !grad_query))
+    return fail(MFA_ERR_INVALID_ARGUMENT, "backwardQuery requires output and gradQuery");
+  if ((phase & PHASE_KV) && (!grad_key || !grad_value))
+    return fail(MFA_ERR_INVALID_ARGUMENT, "backwardKeyValue requires gradKey and gradValue");
+  const mfa_attention_descriptor_t& base = desc->base;
+  if (!base.has_matrix_dimensions) return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
+  const int B = desc->batch_size ? (int)desc->batch_size : 1;
+  const int H = desc->num_heads ? (int)desc->num_heads : 1;
+  const int Hkv = desc->num_kv_heads ? (int)desc->num_kv_heads : H;
+  const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
+  const int DP = pad_head(D);
+  if (DP < 0 || D <= 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d", D);
+  const mfa_quantized_configuration_t& cfg = desc->config;
+  const int qp = cfg.query_precision, kp = cfg.key_precision, vp = cfg.value_precision;
+  int elem = -1;
+  for (int pz : {qp, kp, vp}) {
+    if (!is_quantized(pz)) {
+      const int e = elem_of(pz);
+      if (elem >= 0 && e != elem) return fail(MFA_ERR_UNSUPPORTED, "mixed floating-point input precisions");
+      elem = e;
+    }
+  }
+  if (elem < 0) elem = 1;
+  if (src_kind(kp) != src_kind(vp))
+    return fail(MFA_ERR_UNSUPPORTED, "K and V must share a precision class");
+  if (elem == 0 && (is_quantized(qp) || is_quantized(kp)))
+    return fail(MFA_ERR_UNSUPPORTED, "FP32 query with quantized K/V");
+  const Precisions pr = resolve_precisions(base);
+  if (elem == 0 && pr.mem[MFA_OPERAND_dO] != MFA_PRECISION_FP32)
+    return fail(MFA_ERR_UNSUPPORTED, "FP32 kernels need FP32 dO");
+  if (elem != 0 && pr.mem[MFA_OPERAND_dO] != MFA_PRECISION_FP32 &&
+      elem_of(pr.mem[MFA_OPERAND_dO]) != elem)
+    return fail(MFA_ERR_UNSUPPORTED, "dO precision must be FP32 or the input precision");
+
+  mfa::BwdParams p;
+  memset(&p, 0, sizeof(p));
+  float fq = 1.f, fk = 1.f, fv = 1.f;
+  mfa_status_t st;
+  if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv)) != MFA_SUCCESS) return st;
+  p.dO_op = make_operand(grad_output, pr.mem[MFA_OPERAND_dO], B, H, R, D, nullptr, 0);
+  p.o = output;
+  p.l = logsumexp;
+  p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+  p.dD = d_values;
+  p.d_bf16 = pr.mem[MFA_OPERAND_D] == MFA_PRECISION_BF16;
+  p.dq = grad_query;
+  p.dk = grad_key;
+  p.dv = grad_value;
+  p.B = B; p.H = H; p.Hkv = Hkv; p.R = R; p.C = C; p.D = D;
+  p.group = H / Hkv;
+  const float scale = resolve_scale(base, D);
+  p.c_log2 = 1.442695041f * scale * fq * fk;
+  p.scale = scale * fv;
+  p.dscale = scale;
+  p.dq_mul = fk;
+  p.dk_mul = fq;
+  if ((st = plan_masks(base, nullptr, R, C, &p.mask)) != MFA_SUCCESS) return st;
+  return run_backward(p, elem, DP, src_kind(kp), src_kind(qp), phase, (hipStream_t)stream);
+}
+
+}  // namespace
+
+extern "C" mfa_status_t mfa_quantized_backward_query(
+    const mfa_quantized_descriptor_t* desc, const mfa_quantized_tensor_t* query,
+    const mfa_quantized_tensor_t* key, const mfa_quantized_tensor_t* value, const float* output,
+    const void* grad_output, const void* logsumexp, float* grad_query, void* d_values,
+    void* stream) {
+  return quantized_backward(desc, query, key, value, output, grad_output, logsumexp, grad_query,
+                            nullptr, nullptr, d_values, PHASE_QUERY, stream);
+}
+
+extern "C" mfa_status_t mfa_quantized_backward_key_value(
+    const mfa_quantized_descriptor_t* desc, const mfa_quantized_tensor_t* query,
+    const mfa_quantized_tensor_t* key, const mfa_quantized_tensor_t* value,
+    const void* grad_output, const void* logsumexp, const void* d_values, float* grad_key,
+    float* grad_value, void* stream) {
+  return quantized_backward(desc, query, key, value, nullptr, grad_output, logsumexp, nullptr,
+                            grad_key, grad_value, (void*)d_values, PHASE_KV, stream);
+}

@@ -1,0 +1,52 @@
+// mfa_dispatch.h — compile-time block configurations per kernel instantiation and the
+// host-callable dispatch entry points of each kernel family.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "mfa_params.h"
+
+namespace mfa {
+
+template <class E, int DP> struct Arith16;
+template <int DP> struct Arith32;
+struct F16;
+struct BF16;
+
+template <int ELEM, int DP> struct ArithOf;
+template <int DP> struct ArithOf<1, DP> { using type = Arith16<F16, DP>; };
+template <int DP> struct ArithOf<2, DP> { using type = Arith16<BF16, DP>; };
+template <int DP> struct ArithOf<0, DP> { using type = Arith32<DP>; };
+
+// Forward: NW waves x 32 queries per workgroup, BK keys per K/V tile.
+template <int ELEM, int DP> struct FwdCfg {
+  static constexpr int BK = (ELEM == 0 || DP >= 256) ? 32 : 64;
+  static constexpr int NW = 4;
+};
+// Backward (both phases): NW waves x 32 rows per workgroup, BT rows per traversal tile.
+template <int ELEM, int DP> struct BwdCfg {
+  static constexpr int BT = (ELEM == 0 || DP >= 128) ? 32 : 64;
+  static constexpr int NW = 4;
+};
+
+inline void fwd_block_config(int elem, int DP, int* bq, int* bk, int* nw) {
+  const int BK = (elem == 0 || DP >= 256) ? 32 : 64;
+  *bq = 4 * 32; *bk = BK; *nw = 4;
+}
+inline int fwd_lds_bytes(int elem, int DP) {
+  int bq, bk, nw; fwd_block_config(elem, DP, &bq, &bk, &nw);
+  const int tile = elem == 0 ? bk * (DP + 1) * 4 : bk * DP * 2;
+  return 4 * tile;
+}
+inline void bwd_block_config(int elem, int DP, int* bp, int* bt, int* nw) {
+  const int BT = (elem == 0 || DP >= 128) ? 32 : 64;
+  *bp = 4 * 32; *bt = BT; *nw = 4;
+}
+
+hipError_t fwd_dispatch(const FwdParams& p, int elem, int DP, int ksrc, int vsrc,
+                        hipStream_t stream);
+hipError_t bwd_q_dispatch(const BwdParams& p, int elem, int DP, int ksrc, int vsrc,
+                          hipStream_t stream);
+hipError_t bwd_kv_dispatch(const BwdParams& p, int elem, int DP, int ksrc, int vsrc,
+                           hipStream_t stream);
+int bwd_lds_bytes(int kind, int elem, int DP);
+
+}  // namespace mfa

@@ -1,0 +1,66 @@
+// mfa_params.h — kernel argument structs shared by the host launcher (mfa_api.cpp) and the
+// HIP kernels.  Plain data only: this is the layout of one kernarg segment per launch.
+#pragma once
+#include <stdint.h>
+
+namespace mfa {
+
+// One operand as a kernel sees it: base pointer + ELEMENT strides in BHSD order
+// (MultiHeadAttention.swift:325-336 passes the same four strides; `sd` generalises the
+// transposed layouts of AttentionKernelDescriptor.transposeState).
+struct Operand {
+  const void* ptr;
+  int64_t sb, sh, ss, sd;
+  int32_t prec;      // storage precision (mfa_precision_t)
+  int32_t vec;       // 16-byte (8-byte for INT8) vector loads are legal for every row
+  float scale;       // per-tensor quantisation scale (1 when folded / not quantised)
+  int32_t zp;        // per-tensor zero point
+  const float* bscale;    // blockwise scales (NULL: per-tensor)
+  const int32_t* bzp;     // blockwise zero points (NULL: zero)
+  int32_t bsize;          // block size (elements) of the 2-D [rows, cols] block grid
+  int32_t bcols;          // ceil(cols / bsize)
+  int32_t cols;           // columns of the 2-D quantisation view (= head dim)
+  int32_t pad0;
+};
+
+struct MaskArgs {
+  int32_t causal;
+  int32_t window;          // sliding window active
+  uint32_t window_size;
+  int32_t skip_ok;         // fully masked causal/window tiles may be skipped exactly
+  const float* amask;      // additive fp32 [B, H, R, C] (added to QK^T before scaling)
+  const uint32_t* ranges;  // uint32x2 [B, H_kv, R] half-open key ranges
+};
+
+struct FwdParams {
+  Operand q, k, v;
+  float* o;
+  int64_t o_sb, o_sh, o_ss;
+  void* l;
+  int32_t l_f16;           // L stored as FP16 (lowPrecisionIntermediates)
+  int32_t B, H, Hkv, R, C, D;
+  int32_t nblk;            // query blocks per (batch, head)
+  float c_log2;            // softmax_scale * log2(e) * folded quant scales of Q and K
+  float o_mul;             // folded quant scale of V
+  MaskArgs mask;
+};
+
+struct BwdParams {
+  Operand q, k, v;
+  const float* o;          // forward output (fp32, dense [B, H, R, D])
+  Operand dO_op;           // dO (input precision, or FP32 for the quantized API)
+  const void* l;  int32_t l_f16;
+  void* dD;       int32_t d_bf16;   // D in memory (FP32 or BF16-truncated)
+  float* dq;  float* dk;  float* dv;
+  int32_t B, H, Hkv, R, C, D;
+  int32_t nblk;            // query blocks (bwd_q) or key blocks (bwd_kv) per slice
+  int32_t group;           // H / Hkv (query heads per kv head)
+  float c_log2;            // softmax_scale * log2(e) * quant(Q) * quant(K)
+  float scale;             // softmax_scale · folded quant(V): dS = P∘(dP_int·scale - D)
+  float dscale;            // softmax_scale (D = dscale · rowsum(dO∘O))
+  float dq_mul;            // quant(K) folded into dQ
+  float dk_mul;            // quant(Q) folded into dK
+  MaskArgs mask;
+};
+
+}  // namespace mfa

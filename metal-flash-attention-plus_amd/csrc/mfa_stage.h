@@ -1,0 +1,261 @@
+// mfa_stage.h — global -> register -> LDS staging of [ROWS][DP] operand tiles, and the
+// per-lane register fragments of operands held for a whole kernel (Q in the forward pass).
+//
+// Staging is split into load() (issue the global loads into registers) and store()
+// (dequantise/convert and write the swizzled LDS image), so a kernel can issue the next
+// tile's loads before its MFMA work and write them after (cdna_hip_programming.md T14).
+//
+// Quantised sources follow the reference's dequantize-on-load semantics
+// (GEMMHeaders.swift:679-808): value = (q - zero_point) * scale, INT4 nibble n -> n - 8 with
+// element 2i in the low nibble (GEMMQuantization.swift:500-515), blockwise scale index
+// (row / bs) * ceil(cols / bs) + col / bs over the 2-D [rows, cols] view
+// (GEMMQuantization.swift:561-575, AttentionKernel+OuterProduct.swift:301-316).
+// A per-tensor scale is folded into the softmax / output multipliers by the host so the
+// staged integers (q - zp) are exact in the 16-bit MFMA operand.
+#pragma once
+#include "mfa_device.h"
+#include "mfa_params.h"
+
+namespace mfa {
+
+// SRC_SAME: storage = MFMA element type.  SRC_I8/SRC_I4: quantised integers.
+// SRC_F32ANY: runtime choice between the MFMA element type and FP32 storage that is rounded
+// to the element type (dO is FP32 in memory unless lowPrecisionInputs,
+// AttentionDescriptor+Precisions.swift:17-26).
+enum SrcKind : int { SRC_SAME = 0, SRC_I8 = 1, SRC_I4 = 2, SRC_F32ANY = 3 };
+
+__device__ __forceinline__ int8_t ld_i4(const uint8_t* base, int64_t e) {
+  const uint8_t byte = base[e >> 1];
+  const int nib = (e & 1) ? (byte >> 4) : (byte & 15);
+  return (int8_t)(nib - 8);
+}
+
+// Dequantised value of quantised element (row2d, col) with integer payload qv.
+__device__ __forceinline__ float dequant(const Operand& op, int qv, int64_t row2d, int col) {
+  if (op.bscale) {
+    const int64_t bi = (row2d / op.bsize) * op.bcols + col / op.bsize;
+    const int zp = op.bzp ? op.bzp[bi] : 0;
+    return (float)(qv - zp) * op.bscale[bi];
+  }
+  return (float)(qv - op.zp);  // per-tensor scale folded by the host
+}
+
+template <class A, int ROWS, int DP, int NT, int SRC>
+struct Stager {
+  static constexpr int CE = 16 / A::ESIZE;   // output elements per 16-byte chunk
+  static constexpr int CPR = DP / CE;        // chunks per row
+  static constexpr int NCH = ROWS * CPR;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  uint4 raw[PER];
+  uint4 raw2[SRC == SRC_F32ANY ? PER : 1];  // upper 16 bytes of an FP32-stored chunk
+
+  __device__ __forceinline__ void load(const Operand& op, int b, int hx, int row0, int nrows,
+                                       int D) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int id = tid + i * NT;
+      const int r = id / CPR, c = id % CPR;
+      const int grow = row0 + r;
+      const int d0 = c * CE;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if ((NCH % NT == 0 || id < NCH) && grow < nrows && d0 < D) {
+        const int64_t rowoff = (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss;
+        if constexpr (SRC == SRC_F32ANY) {
+          if (op.prec == P_FP32) {
+            const float* base = (const float*)op.ptr + rowoff;
+            if (op.vec && d0 + 8 <= D) {
+              v = *reinterpret_cast<const uint4*>(base + d0);
+              raw2[i] = *reinterpret_cast<const uint4*>(base + d0 + 4);
+            } else {
+              uint32_t w[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                w[j] = d0 + j < D ? __builtin_bit_cast(uint32_t, base[(int64_t)(d0 + j) * op.sd]) : 0u;
+              v = make_uint4(w[0], w[1], w[2], w[3]);
+              raw2[i] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+          } else {
+            const uint16_t* p = (const uint16_t*)op.ptr + rowoff;
+            if (op.vec && d0 + 8 <= D) {
+              v = *reinterpret_cast<const uint4*>(p + d0);
+            } else {
+              uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if (d0 + j < D) w[j >> 1] |= (uint32_t)p[(int64_t)(d0 + j) * op.sd] << (16 * (j & 1));
+              v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+          }
+        } else if constexpr (SRC == SRC_SAME) {
+          const char* base = (const char*)op.ptr + rowoff * A::ESIZE;
+          if (op.vec && d0 + CE <= D) {
+            v = *reinterpret_cast<const uint4*>(base + (int64_t)d0 * A::ESIZE);
+          } else {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            if constexpr (A::ESIZE == 2) {
+              const uint16_t* p = (const uint16_t*)base;
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if (d0 + j < D) w[j >> 1] |= (uint32_t)p[(int64_t)(d0 + j) * op.sd] << (16 * (j & 1));
+            } else {
+              const uint32_t* p = (const uint32_t*)base;
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (d0 + j < D) w[j] = p[(int64_t)(d0 + j) * op.sd];
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        } else if constexpr (SRC == SRC_I8) {
+          const int8_t* base = (const int8_t*)op.ptr + rowoff;
+          if (op.vec && d0 + 8 <= D) {
+            const uint2 t = *reinterpret_cast<const uint2*>(base + d0);
+            v.x = t.x; v.y = t.y;
+          } else {
+            uint32_t w[2] = {0u, 0u};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (d0 + j < D) w[j >> 2] |= (uint32_t)(uint8_t)base[(int64_t)(d0 + j) * op.sd] << (8 * (j & 3));
+            v.x = w[0]; v.y = w[1];
+          }
+        } else {  // SRC_I4: element index e -> byte e/2, low nibble = even element
+          const uint8_t* base = (const uint8_t*)op.ptr;
+          uint32_t w = 0u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (d0 + j < D) {
+              const int64_t e = rowoff + (int64_t)(d0 + j) * op.sd;
+              const uint8_t byte = base[e >> 1];
+              const uint32_t nib = (e & 1) ? (byte >> 4) : (byte & 15);
+              w |= nib << (4 * j);
+            } else {
+              w |= 8u << (4 * j);  // decodes to 0
+            }
+          v.x = w;
+        }
+      }
+      raw[i] = v;
+      if constexpr (SRC == SRC_F32ANY) {
+        if (!((NCH % NT == 0 || id < NCH) && grow < nrows && d0 < D)) raw2[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* tile, const Operand& op, int b, int hx, int row0,
+                                        int nrows, int D) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int id = tid + i * NT;
+      if (NCH % NT != 0 && id >= NCH) continue;
+      const int r = id / CPR, c = id % CPR;
+      if constexpr (A::is_f32) {
+        float* t = reinterpret_cast<float*>(tile) + r * (DP + 1) + c * 4;
+        t[0] = __builtin_bit_cast(float, raw[i].x);
+        t[1] = __builtin_bit_cast(float, raw[i].y);
+        t[2] = __builtin_bit_cast(float, raw[i].z);
+        t[3] = __builtin_bit_cast(float, raw[i].w);
+      } else {
+        uint4 out;
+        if constexpr (SRC == SRC_SAME) {
+          out = raw[i];
+        } else if constexpr (SRC == SRC_F32ANY) {
+          if (op.prec == P_FP32) {
+            const uint32_t f[8] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w,
+                                   raw2[i].x, raw2[i].y, raw2[i].z, raw2[i].w};
+            uint32_t w[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              w[jj] = (uint32_t)A::Elem::from_f32(__builtin_bit_cast(float, f[2 * jj])) |
+                      ((uint32_t)A::Elem::from_f32(__builtin_bit_cast(float, f[2 * jj + 1])) << 16);
+            out = make_uint4(w[0], w[1], w[2], w[3]);
+          } else {
+            out = raw[i];
+          }
+        } else {
+          const int grow = row0 + r;
+          const int d0 = c * 8;
+          const bool valid = grow < nrows;
+          const int64_t row2d =
+              ((int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss) / op.cols;
+          uint32_t w[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            uint32_t packed = 0u;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int j = 2 * jj + e;
+              int qv;
+              if constexpr (SRC == SRC_I8) {
+                const uint32_t word = j < 4 ? raw[i].x : raw[i].y;
+                qv = (int)(int8_t)((word >> (8 * (j & 3))) & 0xff);
+              } else {
+                qv = (int)((raw[i].x >> (4 * j)) & 15u) - 8;
+              }
+              float x = 0.f;
+              if (valid && d0 + j < D) x = dequant(op, qv, row2d, d0 + j);
+              packed |= (uint32_t)A::Elem::from_f32(x) << (16 * e);
+            }
+            w[jj] = packed;
+          }
+          out = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *reinterpret_cast<uint4*>(tile + A::TileT::off(r, c)) = out;
+      }
+    }
+  }
+};
+
+// Register fragments of a row operand kept for the whole kernel (B operand of S^T = K·Q^T):
+// lane l holds row `row` (= its query), elements d = KSTEP*s + (KSTEP/2)*h + j.
+template <class A, int DP>
+__device__ __forceinline__ void load_row_frags(typename A::frag (&f)[A::DSTEPS],
+                                               const Operand& op, int b, int hx, int row,
+                                               bool valid, int h, int D) {
+  const int64_t rowoff = (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)row * op.ss;
+  if constexpr (A::is_f32) {
+    const float* base = (const float*)op.ptr + rowoff;
+#pragma unroll
+    for (int s = 0; s < A::DSTEPS; ++s) {
+      const int d = 2 * s + h;
+      f[s] = (valid && d < D) ? base[(int64_t)d * op.sd] : 0.f;
+    }
+  } else {
+    const int64_t row2d = (op.prec == P_INT8 || op.prec == P_INT4) ? rowoff / op.cols : 0;
+#pragma unroll
+    for (int s = 0; s < A::DSTEPS; ++s) {
+      const int d0 = 16 * s + 8 * h;
+      i16x8 v;
+      if (op.prec == P_INT8 || op.prec == P_INT4) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float x = 0.f;
+          if (valid && d0 + j < D) {
+            const int64_t e = rowoff + (int64_t)(d0 + j) * op.sd;
+            const int qv = op.prec == P_INT8 ? (int)((const int8_t*)op.ptr)[e]
+                                             : (int)ld_i4((const uint8_t*)op.ptr, e);
+            x = dequant(op, qv, row2d, d0 + j);
+          }
+          v[j] = (short)A::Elem::from_f32(x);
+        }
+      } else if (op.prec == P_FP32) {
+        const float* base = (const float*)op.ptr + rowoff;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = (short)A::Elem::from_f32((valid && d0 + j < D) ? base[(int64_t)(d0 + j) * op.sd] : 0.f);
+      } else {
+        const uint16_t* base = (const uint16_t*)op.ptr + rowoff;
+        if (valid && op.vec && d0 + 8 <= D) {
+          v = *reinterpret_cast<const i16x8*>(base + d0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = (valid && d0 + j < D) ? (short)base[(int64_t)(d0 + j) * op.sd] : (short)0;
+        }
+      }
+      f[s] = v;
+    }
+  }
+}
+
+}  // namespace mfa
