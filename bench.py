@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Headline benchmark: attention TFLOPS/GPU (fwd, seq=4096, d=128), fp16 vs INT8.
+
+Workload (BASELINE.json configs[1]): fp16 forward, B=1 per GPU, H=16, S=4096, D=128, causal,
+O fp32 (the reference's output layout).  One step = one forward pass over the batch through
+the C ABI (mfa_multihead_forward).  Multi-GPU: one process per GPU, batch x head sharded
+with no collective on the data path; each rank runs its own batch element (weak scaling).
+FLOPs are algorithmic: 4·D per unmasked (query, key) pair.
+
+Also reported (same JSON line): the INT8-K/V path and the fp16 path at configs[2]'s shape
+(H16 S8192 D128, non-causal) and their ratio; the kernel's MFMA roofline fraction measured
+live with HIP events on the launch stream; the CPU oracle timed on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+_REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(_REPO, "metal-flash-attention-plus_amd", "python"))
+
+# gfx950 dense fp16/bf16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
+# (MI355X_MICROARCH.md: v_mfma_f32_32x32x16_f16 = 32768 FLOP per 32 cycles per SIMD).
+PEAK_FP16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # 2516.6
+PEAK_INT8_TOPS = 2 * PEAK_FP16_TFLOPS
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--heads", type=int, default=16)
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--no-int8", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import mfa_amd as mfa
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    H, S, D = args.heads, args.seq, args.dim
+    B = 1  # per rank
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+
+    def uniform(shape, dtype):
+        return ((torch.rand(shape, generator=g, device=dev) * 2 - 1) * 0.25).to(dtype)
+
+    # ---------------------------------------------------------------- headline: C2
+    q, k, v = (uniform((B, H, S, D), torch.float16) for _ in range(3))
+    o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+    l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16,
+                                        causal=True)
+    desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+    mha = mfa.MultiHeadAttention()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        mha.forward(desc, q, k, v, o, l, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel per step on this stream
+    flops_step = mfa.attention_flops(B, H, S, S, D, causal=True)
+    total_flops = flops_step * args.steps * world
+    value = total_flops / elapsed / 1e12
+    achieved = flops_step / (kernel_ms * 1e-3) / 1e12
+
+    result = {
+        "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
+        "value": round(value, 2),
+        "unit": "TFLOPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp16",
+        "data": "synthetic (uniform [-0.25, 0.25), device RNG)",
+        "config": {"workload": "fp16 fwd causal, O fp32, L fp16 (BASELINE configs[1])",
+                   "batch_per_gpu": B, "heads": H, "seq_len": S, "head_dim": D,
+                   "parallelism": f"batch-sharded x{world}, no collective",
+                   "flop_convention": "4*D per unmasked pair (causal S(S+1)/2)",
+                   "gflop_per_step_per_gpu": round(flops_step / 1e9, 3)},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
+                     "peak": round(PEAK_FP16_TFLOPS, 1), "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": None,
+                     "kernel": "mfa_fwd_kernel<Arith16<F16,128>,128,64,4,0,0>",
+                     "kernel_ms": round(kernel_ms, 4)},
+    }
+    del q, k, v, o, l
+
+    # ---------------------------------------------------------------- INT8 vs fp16 at C3
+    if not args.no_int8:
+        S3 = 8192
+        qf = uniform((B, H, S3, D), torch.float16)
+        kf = uniform((B, H, S3, D), torch.float32)
+        vf = uniform((B, H, S3, D), torch.float32)
+        o3 = torch.empty((B, H, S3, D), dtype=torch.float32, device=dev)
+        l3 = torch.empty((B, H, S3), dtype=torch.float16, device=dev)
+        kq, ks, _, _ = mfa.quantize(kf, mfa.Precision.INT8, rows=B * H * S3, cols=D)
+        vq, vs, _, _ = mfa.quantize(vf, mfa.Precision.INT8, rows=B * H * S3, cols=D)
+        torch.cuda.synchronize()
+        base3 = mfa.AttentionDescriptor.make(S3, S3, D, low_precision=True,
+                                             precision=mfa.Precision.FP16)
+        qdesc = mfa.quantized_descriptor(base3, mfa.Precision.FP16, mfa.Precision.INT8,
+                                         mfa.Precision.INT8, B=B, H=H)
+        qa = mfa.QuantizedAttention()
+        tq = mfa.quantized_tensor(qf, mfa.Precision.FP16)
+        tk = mfa.quantized_tensor(kq, mfa.Precision.INT8, scale=float(ks.item()))
+        tv = mfa.quantized_tensor(vq, mfa.Precision.INT8, scale=float(vs.item()))
+        kh, vh = kf.half(), vf.half()
+        desc3 = mfa.MultiHeadDescriptor.make(base3, B, H, S3, D)
+
+        def time_it(fn, steps):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / steps
+
+        ms_i8 = time_it(lambda: qa.forward(qdesc, tq, tk, tv, o3, l3, stream=stream),
+                        max(3, args.steps // 4))
+        ms_f16 = time_it(lambda: mha.forward(desc3, qf, kh, vh, o3, l3, stream=stream),
+                         max(3, args.steps // 4))
+        f3 = mfa.attention_flops(B, H, S3, S3, D, causal=False)
+        result["int8"] = {
+            "workload": "INT8 K/V (per-tensor, zp 0) + fp16 Q, H16 S8192 D128 non-causal "
+                        "(BASELINE configs[2]); int8 path = dequant-exact K/V -> fp16 MFMA",
+            "int8_tflops": round(f3 / (ms_i8 * 1e-3) / 1e12, 2),
+            "fp16_tflops_same_shape": round(f3 / (ms_f16 * 1e-3) / 1e12, 2),
+            "ratio_int8_over_fp16": round(ms_f16 / ms_i8, 3),
+            "int8_ms": round(ms_i8, 4), "fp16_ms": round(ms_f16, 4),
+        }
+        del qf, kf, vf, o3, l3, kq, vq, kh, vh
+
+    # ---------------------------------------------------------------- CPU baseline
+    if rank == 0 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(S, D)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(S: int, D: int):
+    """The CPU oracle (C restatement of Network.swift's naive reference) on ONE (batch, head)
+    slice of the headline workload, causal, all host threads (OpenMP over query rows)."""
+    sys.path.insert(0, os.path.join(_REPO, "tests"))
+    import numpy as np
+    import oracle_lib as ol
+    threads = min(16, os.cpu_count() or 1)
+    threads = ol.set_threads(threads)
+    rng = np.random.default_rng(0)
+    q, k, v = ((rng.random((1, 1, S, D), dtype=np.float32) * 2 - 1) * 0.25 for _ in range(3))
+    t0 = time.perf_counter()
+    ol.attention(q, k, v, causal=True)
+    dt = time.perf_counter() - t0
+    flops = 4.0 * D * (S * (S + 1) // 2)
+    return {"value": round(flops / dt / 1e12, 5), "unit": "TFLOPS", "cores": threads,
+            "kind": "port",
+            "sample": f"1 head of the headline workload (S={S}, D={D}, causal), "
+                      f"oracle/mfa_oracle.c forward, {dt:.2f}s; naive row-wise restatement "
+                      "of Network.swift (computes masked columns too, double accumulation)"}
+
+
+if __name__ == "__main__":
+    main()

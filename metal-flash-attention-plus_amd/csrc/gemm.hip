@@ -1,0 +1,197 @@
+// gemm.hip — C[M,N] = A[M,K]·B[K,N] (+ C) on MFMA, the GEMM the reference uses on the hot path
+// only for MLA decompression (MLAOptimizedGEMMMFA.swift:97-154: FP16 NN, K[B·S, H·D] =
+// latent[B·S, 512]·W_k[512, H·D]).  The reference accumulates FP16xFP16 in FP16 registers
+// (GEMMDescriptor.swift:204-210); here accumulation is FP32 and C is rounded once.
+//
+// Tiling: 128x128 output per workgroup of 4 waves (2x2, 64x64 per wave = 2x2 MFMA 32x32
+// tiles), K staged 32 deep through double-buffered LDS.  B is row-major [K][N], so its MFMA
+// operand (8 consecutive k of one column) is read with ds_read_b64_tr_b16; A is then read in
+// the same permuted k order (two 8-byte reads per fragment) so the products pair up.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mfa/mfa.h"
+#include "mfa_device.h"
+#include "mfa_params.h"
+#include "mfa_dispatch.h"
+
+namespace mfa {
+
+template <class E>
+__global__ void __launch_bounds__(256) mfa_gemm_kernel(GemmParams p) {
+  constexpr int BM = 128, BN = 128, BK = 32;
+  using TA = Tile16<BK>;   // [BM][BK]
+  using TB = Tile16<BN>;   // [BK][BN]
+  using AB = Arith16<E, BN>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM * BK * 2 + BK * BN * 2)];
+  char* const ab = smem;
+  char* const bb = smem + 2 * BM * BK * 2;
+  constexpr int ATILE = BM * BK * 2, BTILE = BK * BN * 2;
+
+  const int z = blockIdx.z;
+  const uint16_t* A = (const uint16_t*)p.a + (p.b[1] ? 0 : z * p.sa);
+  const uint16_t* B = (const uint16_t*)(p.b[1] ? p.b[z] : p.b[0]) + (p.b[1] ? 0 : z * p.sb);
+  char* C = (char*)(p.b[1] ? p.c[z] : p.c[0]);
+  const int64_t coff = p.b[1] ? 0 : z * p.sc;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+
+  // Each thread stages 2 A chunks and 2 B chunks (16 bytes = 8 elements each).
+  uint4 ra[2], rb[2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + i * 256;
+      {  // A: 128 rows x 4 chunks
+        const int r = id >> 2, c = id & 3;
+        const int gm = m0 + r, gk = k0 + c * 8;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (gm < p.M) {
+          const uint16_t* src = A + (int64_t)gm * p.lda + gk;
+          if (gk + 8 <= p.K && ((((uintptr_t)src) & 15) == 0)) {
+            v = *reinterpret_cast<const uint4*>(src);
+          } else {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int j = 0; j < 8; ++j)
+              if (gk + j < p.K) w[j >> 1] |= (uint32_t)src[j] << (16 * (j & 1));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        }
+        ra[i] = v;
+      }
+      {  // B: 32 rows x 16 chunks
+        const int r = id >> 4, c = id & 15;
+        const int gk = k0 + r, gn = n0 + c * 8;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (gk < p.K) {
+          const uint16_t* src = B + (int64_t)gk * p.ldb + gn;
+          if (gn + 8 <= p.N && ((((uintptr_t)src) & 15) == 0)) {
+            v = *reinterpret_cast<const uint4*>(src);
+          } else {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int j = 0; j < 8; ++j)
+              if (gn + j < p.N) w[j >> 1] |= (uint32_t)src[j] << (16 * (j & 1));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        }
+        rb[i] = v;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + i * 256;
+      *reinterpret_cast<uint4*>(ab + buf * ATILE + TA::off(id >> 2, id & 3)) = ra[i];
+      *reinterpret_cast<uint4*>(bb + buf * BTILE + TB::off(id >> 4, id & 15)) = rb[i];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+
+  load(0);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < p.K; k0 += BK) {
+    const bool has_next = k0 + BK < p.K;
+    if (has_next) load(k0 + BK);
+    const char* at = ab + cur * ATILE;
+    const char* bt = bb + cur * BTILE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      i16x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // A row (m), k = 16s + 8(j>>2) + 4h + (j&3): the order read_tr produces for B.
+        const int r = wm * 64 + i * 32 + l32;
+        const uint2 lo = *reinterpret_cast<const uint2*>(at + TA::off(r, 2 * s) + 8 * hh);
+        const uint2 hi = *reinterpret_cast<const uint2*>(at + TA::off(r, 2 * s + 1) + 8 * hh);
+        af[i] = __builtin_bit_cast(i16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = AB::read_tr(bt, 0, s, wn * 64 + j * 32, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = E::mma(af[i], bf[j], acc[i][j]);
+    }
+    if (has_next) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // acc[i][j]: column n = lane, rows m = acc_row(r, h).
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + l32;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + acc_row(r, hh);
+        if (m >= p.M) continue;
+        const int64_t ci = coff + (int64_t)m * p.ldc + n;
+        float x = acc[i][j][r];
+        if (p.prec_c == P_FP32) {
+          float* cf = reinterpret_cast<float*>(C);
+          cf[ci] = p.load_prev ? x + cf[ci] : x;
+        } else {
+          uint16_t* ch = reinterpret_cast<uint16_t*>(C);
+          if (p.load_prev) x += (p.prec_c == P_FP16 ? f16_to_f32(ch[ci]) : bf16_to_f32(ch[ci]));
+          ch[ci] = p.prec_c == P_FP16 ? f32_to_f16(x) : f32_to_bf16(x);
+        }
+      }
+    }
+}
+
+hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream) {
+  const dim3 grid((p.N + 127) / 128, (p.M + 127) / 128, batch);
+  if (prec_ab == P_FP16)
+    hipLaunchKernelGGL(mfa_gemm_kernel<F16>, grid, dim3(256), 0, stream, p);
+  else if (prec_ab == P_BF16)
+    hipLaunchKernelGGL(mfa_gemm_kernel<BF16>, grid, dim3(256), 0, stream, p);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace mfa
+
+extern "C" mfa_status_t mfa_gemm(const mfa_gemm_descriptor_t* d, const void* A, const void* B,
+                                 void* C, void* stream) {
+  using namespace mfa;
+  if (!d || !A || !B || !C) return MFA_ERR_INVALID_ARGUMENT;
+  if (d->transpose_a || d->transpose_b) return MFA_ERR_UNSUPPORTED;
+  if (d->precision_a != d->precision_b ||
+      (d->precision_a != MFA_PRECISION_FP16 && d->precision_a != MFA_PRECISION_BF16))
+    return MFA_ERR_UNSUPPORTED;
+  if (d->precision_c != MFA_PRECISION_FP32 && d->precision_c != MFA_PRECISION_FP16 &&
+      d->precision_c != MFA_PRECISION_BF16)
+    return MFA_ERR_UNSUPPORTED;
+  if (d->M == 0 || d->N == 0) return MFA_SUCCESS;
+  GemmParams p{};
+  p.a = A;
+  p.b[0] = B;
+  p.b[1] = nullptr;
+  p.c[0] = C;
+  p.M = (int)d->M; p.N = (int)d->N; p.K = (int)d->K;
+  p.lda = d->lda ? (int)d->lda : (int)d->K;
+  p.ldb = d->ldb ? (int)d->ldb : (int)d->N;
+  p.ldc = d->ldc ? (int)d->ldc : (int)d->N;
+  p.sa = (int64_t)d->stride_a; p.sb = (int64_t)d->stride_b; p.sc = (int64_t)d->stride_c;
+  p.prec_c = d->precision_c;
+  p.load_prev = d->load_previous_c;
+  const int batch = d->batch ? (int)d->batch : 1;
+  return gemm_dispatch(p, d->precision_a, batch, (hipStream_t)stream) == hipSuccess
+             ? MFA_SUCCESS
+             : MFA_ERR_LAUNCH;
+}

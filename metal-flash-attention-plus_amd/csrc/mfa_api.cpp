@@ -787,3 +787,74 @@ extern "C" mfa_status_t mfa_quantized_backward_key_value(
   return quantized_backward(desc, query, key, value, nullptr, grad_output, logsumexp, nullptr,
                             grad_key, grad_value, (void*)d_values, PHASE_KV, stream);
 }
+
+// =========================================================================================
+// MLA (MLAOptimizedGEMMMFA.forward, MLAOptimizedGEMMMFA.swift:158-240) + the attention forward
+// its caller runs on the decompressed BSHD K/V (stride pattern KernelRegressionTests.swift:
+// 398-465).
+extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const void* kv_latent,
+                                        const void* w_k, const void* w_v, const void* query,
+                                        void* decompressed_k, void* decompressed_v,
+                                        float* output, void* logsumexp, void* stream) {
+  if (!desc || !kv_latent || !w_k || !w_v || !query || !output)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "MLA forward requires latent, weights, query, output");
+  const int prec = desc->precision;
+  if (prec != MFA_PRECISION_FP16 && prec != MFA_PRECISION_BF16)
+    return fail(MFA_ERR_UNSUPPORTED, "MLA precision must be FP16 or BF16");
+  const int B = (int)desc->batch_size, H = (int)desc->num_heads;
+  const int Sq = (int)desc->sequence_length_q, Skv = (int)desc->sequence_length_kv;
+  const int D = (int)desc->head_dim, Lat = (int)desc->kv_latent_dim;
+  if (B <= 0 || H <= 0 || D <= 0 || Lat <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "empty MLA shape");
+  const int DP = pad_head(D);
+  if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", D);
+  const int64_t kv_elems = (int64_t)B * Skv * H * D;
+  hipStream_t s = (hipStream_t)stream;
+  mfa_status_t st;
+  void* kb = decompressed_k;
+  void* vb = decompressed_v;
+  if (!kb || !vb) {
+    void* both = nullptr;
+    if ((st = scratch((size_t)kv_elems * 2 * 2, &both, 1)) != MFA_SUCCESS) return st;
+    kb = both;
+    vb = (char*)both + kv_elems * 2;
+  }
+  // K = latent · W_k and V = latent · W_v in one launch (grid z = 2).
+  mfa::GemmParams g;
+  memset(&g, 0, sizeof(g));
+  g.a = kv_latent;
+  g.b[0] = w_k; g.b[1] = w_v;
+  g.c[0] = kb; g.c[1] = vb;
+  g.M = B * Skv; g.N = H * D; g.K = Lat;
+  g.lda = Lat; g.ldb = H * D; g.ldc = H * D;
+  g.prec_c = prec;
+  if (B * Skv > 0) {
+    st = hip_status(mfa::gemm_dispatch(g, prec, 2, s), "mfa_gemm (MLA decompress) launch");
+    if (st != MFA_SUCCESS) return st;
+  }
+  if (Sq == 0) return MFA_SUCCESS;
+  // Attention on BSHD K/V: element strides [S·H·D, D, H·D, 1].
+  const int64_t kv_strides[4] = {(int64_t)Skv * H * D, D, (int64_t)H * D, 1};
+  mfa::FwdParams p;
+  memset(&p, 0, sizeof(p));
+  p.q = make_operand(query, prec, B, H, Sq, D, nullptr, 0);
+  p.k = make_operand(kb, prec, B, H, Skv, D, kv_strides, 0);
+  p.v = make_operand(vb, prec, B, H, Skv, D, kv_strides, 0);
+  p.o = output;
+  p.o_ss = D; p.o_sh = (int64_t)Sq * D; p.o_sb = (int64_t)H * Sq * D;
+  const Precisions pr = resolve_precisions(desc->base);
+  p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+  void* L = logsumexp;
+  if (!L) {
+    if ((st = scratch((size_t)B * H * Sq * 4, &L, 0)) != MFA_SUCCESS) return st;
+  }
+  p.l = L;
+  p.B = B; p.H = H; p.Hkv = H; p.R = Sq; p.C = Skv; p.D = D;
+  const int elem = elem_of(prec);
+  int bq, bk, nw;
+  mfa::fwd_block_config(elem, DP, &bq, &bk, &nw);
+  p.nblk = (Sq + bq - 1) / bq;
+  p.c_log2 = 1.442695041f * resolve_scale(desc->base, D);
+  p.o_mul = 1.f;
+  if ((st = plan_masks(desc->base, nullptr, Sq, Skv, &p.mask)) != MFA_SUCCESS) return st;
+  return hip_status(mfa::fwd_dispatch(p, elem, DP, 0, 0, s), "mfa_fwd (MLA) launch");
+}

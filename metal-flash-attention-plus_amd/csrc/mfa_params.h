@@ -63,4 +63,16 @@ struct BwdParams {
   MaskArgs mask;
 };
 
+// MFMA GEMM (gemm.hip): C = A·B (+C); two (B, C) pairs share A when b[1] != nullptr.
+struct GemmParams {
+  const void* a;
+  const void* b[2];
+  void* c[2];
+  int32_t M, N, K;
+  int32_t lda, ldb, ldc;
+  int64_t sa, sb, sc;     // batch strides (elements) when b[1] == nullptr
+  int32_t prec_c;         // P_FP32 / P_FP16 / P_BF16
+  int32_t load_prev;
+};
+
 }  // namespace mfa

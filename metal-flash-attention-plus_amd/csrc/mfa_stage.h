@@ -40,6 +40,56 @@ __device__ __forceinline__ float dequant(const Operand& op, int qv, int64_t row2
   return (float)(qv - op.zp);  // per-tensor scale folded by the host
 }
 
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// 8 quantised elements (INT8 in raw.x/raw.y, or 8 INT4 nibbles in raw.x) -> 8 MFMA elements
+// holding q - zp.  FP16: build 1024 + u in the fp16 bit pattern (0x6400 | u, u = q + 128 via
+// v_perm_b32) and subtract 1152 + zp with packed fp16 math — exact for |q - zp| <= 1024.
+template <class E, int SRC>
+__device__ __forceinline__ uint4 dequant_fast(const uint4 raw, float zp) {
+  uint32_t w[4];
+  if constexpr (E::prec == P_FP16) {
+    if constexpr (SRC == SRC_I8) {
+      const uint32_t u0 = raw.x ^ 0x80808080u, u1 = raw.y ^ 0x80808080u;
+      w[0] = __builtin_amdgcn_perm(0x64646464u, u0, 0x04010400u);
+      w[1] = __builtin_amdgcn_perm(0x64646464u, u0, 0x04030402u);
+      w[2] = __builtin_amdgcn_perm(0x64646464u, u1, 0x04010400u);
+      w[3] = __builtin_amdgcn_perm(0x64646464u, u1, 0x04030402u);
+      const _Float16 m = (_Float16)(1152.0f + zp);
+      const f16x2 mm = {m, m};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
+    } else {  // INT4 nibble n encodes n - 8
+      const uint32_t x = raw.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = 0x64006400u | ((x >> (8 * k)) & 0xFu) | (((x >> (8 * k + 4)) & 0xFu) << 16);
+      const _Float16 m = (_Float16)(1032.0f + zp);
+      const f16x2 mm = {m, m};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int q0, q1;
+      if constexpr (SRC == SRC_I8) {
+        const uint32_t word = k < 2 ? raw.x : raw.y;
+        q0 = (int)(int8_t)(word >> (16 * (k & 1)));
+        q1 = (int)(int8_t)(word >> (16 * (k & 1) + 8));
+      } else {
+        q0 = (int)((raw.x >> (8 * k)) & 15u) - 8;
+        q1 = (int)((raw.x >> (8 * k + 4)) & 15u) - 8;
+      }
+      w[k] = (uint32_t)E::from_f32((float)q0 - zp) | ((uint32_t)E::from_f32((float)q1 - zp) << 16);
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 template <class A, int ROWS, int DP, int NT, int SRC>
 struct Stager {
   static constexpr int CE = 16 / A::ESIZE;   // output elements per 16-byte chunk
@@ -172,6 +222,10 @@ struct Stager {
           } else {
             out = raw[i];
           }
+        } else if (!op.bscale) {
+          // Per-tensor: the staged value is the exact integer (q - zp); zero-filled loads
+          // beyond the tile edge only ever meet zero Q columns or masked keys.
+          out = dequant_fast<typename A::Elem, SRC>(raw[i], (float)op.zp);
         } else {
           const int grow = row0 + r;
           const int d0 = c * 8;

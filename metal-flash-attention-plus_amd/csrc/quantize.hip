@@ -1,0 +1,222 @@
+// quantize.hip — GPU runtime quantisation, bit-exact with the reference's CPU quantiser
+// (Sources/FlashAttention/GEMM/GEMMQuantization.swift):
+//   tensor-wise  scale = absmax/127 (INT8) or absmax/7 (INT4), zero point 0      (:305-350)
+//   block-wise   one scale per 2-D bs x bs block, row-major block order          (:353-421)
+//   row-wise     one scale per row                                              (:424-479)
+//   INT8  q = Int8(clamping: Int32(round(x / scale)) + zp)                       (:487-499)
+//   INT4  nibble = clamp(q + 8, 0, 15), element 2i in the low nibble of byte i;  (:500-516)
+//         tensor-wise pads an odd tail with nibble 8, block-wise with 0          (:600-619)
+// The reference runs this on the host per call (QuantizedTensor.from, :720-860; GPU kernels in
+// GEMMRuntimeQuantization.metal are only loaded when a default library exists).  Here the
+// reduction and the element pass run on the device: absmax reductions are order-independent
+// and the per-element arithmetic is IEEE division + round-half-away, so bytes and scales match
+// the CPU oracle exactly.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mfa/mfa.h"
+#include "mfa_device.h"
+
+namespace mfa {
+
+__device__ __forceinline__ float load_any(const void* p, int prec, uint64_t i) {
+  switch (prec) {
+    case P_FP32: return reinterpret_cast<const float*>(p)[i];
+    case P_FP16: return f16_to_f32(reinterpret_cast<const uint16_t*>(p)[i]);
+    default: return bf16_to_f32(reinterpret_cast<const uint16_t*>(p)[i]);
+  }
+}
+
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+
+// |x| as an order-preserving unsigned key (NaN-free inputs).
+__device__ __forceinline__ unsigned abs_bits(float x) {
+  return __builtin_bit_cast(unsigned, x) & 0x7fffffffu;
+}
+
+__global__ void qz_absmax_tensor(const void* in, int prec, uint64_t n, unsigned* ws) {
+  float m = 0.f;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(load_any(in, prec, i)));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(ws, abs_bits(m));
+}
+
+__global__ void qz_scale_tensor(const unsigned* ws, float* scale_out, float div) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) scale_out[0] = __builtin_bit_cast(float, ws[0]) / div;
+}
+
+// One workgroup per group: block (br, bc) of bsr x bsc elements, or a row (bsr = 1, bsc = cols).
+__global__ void qz_absmax_groups(const void* in, int prec, uint64_t n, uint32_t rows,
+                                 uint32_t cols, uint32_t bsr, uint32_t bsc, uint32_t nbc,
+                                 float* scales, int32_t* zps, float div) {
+  __shared__ float red[16];
+  const uint32_t g = blockIdx.x;
+  const uint32_t br = g / nbc, bc = g % nbc;
+  const uint64_t r0 = (uint64_t)br * bsr, c0 = (uint64_t)bc * bsc;
+  const uint64_t r1 = r0 + bsr < rows ? r0 + bsr : rows;
+  const uint64_t c1 = c0 + bsc < cols ? c0 + bsc : cols;
+  const uint64_t w = c1 - c0, cnt = (r1 - r0) * w;
+  float m = 0.f;
+  for (uint64_t t = threadIdx.x; t < cnt; t += blockDim.x) {
+    const uint64_t idx = (r0 + t / w) * cols + c0 + t % w;
+    if (idx < n) m = fmaxf(m, fabsf(load_any(in, prec, idx)));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mm = 0.f;
+    for (uint32_t i = 0; i < blockDim.x / 64; ++i) mm = fmaxf(mm, red[i]);
+    scales[g] = mm / div;
+    if (zps) zps[g] = 0;  // symmetric quantisation (GEMMQuantization.swift:410)
+  }
+}
+
+__device__ __forceinline__ int32_t round_to_int(float v) {
+  const float r = roundf(v);  // Swift round: half away from zero
+  if (!(r == r)) return 0;
+  if (r >= 2147483647.0f) return 2147483647;
+  if (r <= -2147483648.0f) return (-2147483647 - 1);
+  return (int32_t)r;
+}
+__device__ __forceinline__ int8_t clamp8(int64_t v) {
+  return (int8_t)(v < -128 ? -128 : (v > 127 ? 127 : v));
+}
+__device__ __forceinline__ uint32_t nib(int64_t v) {
+  return (uint32_t)(v < 0 ? 0 : (v > 15 ? 15 : v));
+}
+
+// mode 0 tensor-wise (scale_t[0]), 1 block-wise / 2 row-wise (scales[group]).
+__global__ void qz_quantize(const void* in, int prec, uint64_t n, uint32_t cols, int target,
+                            int mode, uint32_t bs, uint32_t nbc, const float* scale_t,
+                            const float* scales, uint8_t* out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  auto group = [&](uint64_t i) -> uint64_t {
+    const uint64_t r = i / cols, c = i % cols;
+    return mode == 1 ? (r / bs) * nbc + c / bs : r;
+  };
+  if (target == P_INT8) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+      const float s = mode == 0 ? scale_t[0] : scales[group(i)];
+      reinterpret_cast<int8_t*>(out)[i] = clamp8((int64_t)round_to_int(load_any(in, prec, i) / s));
+    }
+  } else {
+    const uint64_t nbytes = (n + 1) / 2;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nbytes; t += stride) {
+      const uint64_t i = 2 * t;
+      const float s0 = mode == 0 ? scale_t[0] : scales[group(i)];
+      const uint32_t lo = nib((int64_t)round_to_int(load_any(in, prec, i) / s0) + 8);
+      uint32_t hi;
+      if (i + 1 < n) {
+        const float s1 = mode == 0 ? scale_t[0] : scales[group(i + 1)];
+        hi = nib((int64_t)round_to_int(load_any(in, prec, i + 1) / s1) + 8);
+      } else {
+        hi = mode == 0 ? 8u : 0u;
+      }
+      out[t] = (uint8_t)((hi << 4) | lo);
+    }
+  }
+}
+
+__global__ void qz_dequantize(const uint8_t* in, int prec, uint64_t n, uint32_t cols, float scale,
+                              int32_t zp, const float* bscale, const int32_t* bzp, uint32_t bs,
+                              uint32_t nbc, float* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const int32_t q = prec == P_INT8 ? (int32_t)reinterpret_cast<const int8_t*>(in)[i]
+                                     : (int32_t)((i & 1) ? (in[i / 2] >> 4) : (in[i / 2] & 15)) - 8;
+    if (bscale) {
+      const uint64_t b = (i / cols / bs) * nbc + (i % cols) / bs;
+      out[i] = ((float)q - (float)(bzp ? bzp[b] : 0)) * bscale[b];
+    } else {
+      out[i] = ((float)q - (float)zp) * scale;
+    }
+  }
+}
+
+}  // namespace mfa
+
+namespace {
+thread_local char g_qerr[256];
+int grid_for(uint64_t n) {
+  const uint64_t g = (n + 255) / 256;
+  return (int)(g < 8192 ? (g == 0 ? 1 : g) : 8192);
+}
+}  // namespace
+
+extern "C" size_t mfa_quantize_workspace_size(uint64_t count, uint32_t rows, uint32_t cols,
+                                              int32_t mode, uint32_t block_size) {
+  (void)count; (void)rows; (void)cols; (void)block_size;
+  return mode == MFA_QUANT_TENSOR_WISE ? 16 : 0;
+}
+
+extern "C" mfa_status_t mfa_quantize(const void* input, int32_t input_precision, uint64_t count,
+                                     uint32_t rows, uint32_t cols, int32_t target_precision,
+                                     int32_t mode, uint32_t block_size, void* output,
+                                     float* scale_out, float* block_scales_out,
+                                     int32_t* block_zero_points_out, void* workspace,
+                                     void* stream) {
+  using namespace mfa;
+  if (!input || !output) return MFA_ERR_INVALID_ARGUMENT;
+  if (input_precision != MFA_PRECISION_FP32 && input_precision != MFA_PRECISION_FP16 &&
+      input_precision != MFA_PRECISION_BF16)
+    return MFA_ERR_UNSUPPORTED;
+  if (target_precision != MFA_PRECISION_INT8 && target_precision != MFA_PRECISION_INT4)
+    return MFA_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const float div = target_precision == MFA_PRECISION_INT8 ? 127.0f : 7.0f;
+  if (count == 0) return MFA_SUCCESS;
+  if (mode == MFA_QUANT_TENSOR_WISE) {
+    if (!workspace || !scale_out) return MFA_ERR_INVALID_ARGUMENT;
+    if (hipMemsetAsync(workspace, 0, 16, s) != hipSuccess) return MFA_ERR_LAUNCH;
+    hipLaunchKernelGGL(qz_absmax_tensor, dim3(grid_for(count)), dim3(256), 0, s, input,
+                       input_precision, count, (unsigned*)workspace);
+    hipLaunchKernelGGL(qz_scale_tensor, dim3(1), dim3(64), 0, s, (const unsigned*)workspace,
+                       scale_out, div);
+    hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
+                       input_precision, count, cols ? cols : 1u, target_precision, 0, 1u, 1u,
+                       (const float*)scale_out, (const float*)nullptr, (uint8_t*)output);
+  } else if (mode == MFA_QUANT_BLOCKWISE || mode == MFA_QUANT_ROW_WISE) {
+    if (!block_scales_out || rows == 0 || cols == 0) return MFA_ERR_INVALID_ARGUMENT;
+    uint32_t bsr, bsc, nbr, nbc;
+    if (mode == MFA_QUANT_BLOCKWISE) {
+      if (block_size == 0) return MFA_ERR_INVALID_ARGUMENT;
+      bsr = bsc = block_size;
+      nbr = (rows + block_size - 1) / block_size;
+      nbc = (cols + block_size - 1) / block_size;
+    } else {
+      bsr = 1; bsc = cols; nbr = rows; nbc = 1;
+    }
+    hipLaunchKernelGGL(qz_absmax_groups, dim3(nbr * nbc), dim3(256), 0, s, input, input_precision,
+                       count, rows, cols, bsr, bsc, nbc, block_scales_out, block_zero_points_out,
+                       div);
+    hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
+                       input_precision, count, cols, target_precision,
+                       mode == MFA_QUANT_BLOCKWISE ? 1 : 2, block_size ? block_size : 1u, nbc,
+                       (const float*)nullptr, (const float*)block_scales_out, (uint8_t*)output);
+  } else {
+    return MFA_ERR_INVALID_DESCRIPTOR;
+  }
+  return hipGetLastError() == hipSuccess ? MFA_SUCCESS : MFA_ERR_LAUNCH;
+}
+
+extern "C" mfa_status_t mfa_dequantize(const mfa_quantized_tensor_t* t, uint64_t count,
+                                       uint32_t cols, float* output, void* stream) {
+  using namespace mfa;
+  if (!t || !t->data || !output) return MFA_ERR_INVALID_ARGUMENT;
+  if (t->precision != MFA_PRECISION_INT8 && t->precision != MFA_PRECISION_INT4)
+    return MFA_ERR_UNSUPPORTED;
+  if (count == 0) return MFA_SUCCESS;
+  const uint32_t bs = t->block_size ? t->block_size : 1u;
+  const uint32_t c = cols ? cols : 1u;
+  hipLaunchKernelGGL(qz_dequantize, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)t->data, t->precision, count, c, t->scale, t->zero_point,
+                     t->block_scales, t->block_zero_points, bs, (c + bs - 1) / bs, output);
+  return hipGetLastError() == hipSuccess ? MFA_SUCCESS : MFA_ERR_LAUNCH;
+}

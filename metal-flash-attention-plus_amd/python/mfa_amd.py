@@ -464,6 +464,7 @@ def quantized_tensor(data, precision: Precision, scale=1.0, zero_point=0, block_
     t.block_scales = _ptr(block_scales)
     t.block_zero_points = _ptr(block_zero_points)
     t.block_size = int(block_size)
+    t._keep = (data, block_scales, block_zero_points)  # the struct holds raw device pointers
     return t
 
 

@@ -1,0 +1,97 @@
+"""GPU parity for the MLA path (MLAOptimizedGEMMMFA.forward + attention on the decompressed BSHD
+K/V) and the MFMA GEMM it uses.  The reference has no MLA test (parity unpinned):
+the pin here is the oracle's fp32-accumulated GEMM followed by the attention oracle, with the
+decompressed K/V rounded to the working precision as the kernel stores them."""
+import numpy as np
+import pytest
+import torch
+
+import mfa_amd as mfa
+import oracle_lib as ol
+from harness import maxerr, relerr, seen, to_device
+
+pytestmark = pytest.mark.gpu
+P = mfa.Precision
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("prec", [P.FP16, P.BF16])
+@pytest.mark.parametrize("out", [P.FP32, "same"])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (130, 70, 33), (512, 384, 512), (1, 9, 5)])
+def test_gemm(gpu, prec, out, M, N, K):
+    out = prec if out == "same" else out
+    rng = np.random.default_rng(M + N + K)
+    A = seen(rng.standard_normal((M, K)).astype(np.float32), prec)
+    B = seen(rng.standard_normal((K, N)).astype(np.float32), prec)
+    C = torch.full((M, N), float("nan"), dtype=torch.float32 if out == P.FP32 else
+                   (torch.float16 if prec == P.FP16 else torch.bfloat16), device=DEV)
+    mfa.gemm(to_device(A, prec), to_device(B, prec), C, M, N, K, prec, out)
+    torch.cuda.synchronize()
+    ref = ol.gemm(A, B)
+    if out != P.FP32:
+        ref = seen(ref, prec)
+    tol = 1e-3 * np.sqrt(K) if out == P.FP32 else (1e-2 if prec == P.FP16 else 4e-2) * np.abs(ref).max()
+    assert maxerr(C, ref) <= tol
+
+
+def test_gemm_batched_and_accumulate(gpu):
+    rng = np.random.default_rng(2)
+    Bn, M, N, K = 3, 70, 96, 40
+    A = seen(rng.standard_normal((Bn, M, K)).astype(np.float32), P.FP16)
+    Bm = seen(rng.standard_normal((Bn, K, N)).astype(np.float32), P.FP16)
+    C0 = rng.standard_normal((Bn, M, N)).astype(np.float32)
+    C = torch.from_numpy(C0.copy()).to(DEV)
+    mfa.gemm(to_device(A, P.FP16), to_device(Bm, P.FP16), C, M, N, K, P.FP16, P.FP32,
+             load_previous_c=True, batch=Bn, stride_a=M * K, stride_b=K * N, stride_c=M * N)
+    torch.cuda.synchronize()
+    ref = np.stack([ol.gemm(A[i], Bm[i]) for i in range(Bn)]) + C0
+    assert maxerr(C, ref) <= 1e-3 * np.sqrt(K)
+
+
+def run_mla(B, H, S, D, latent, prec, causal=False, seed=0):
+    rng = np.random.default_rng(seed)
+    lat = seen(rng.standard_normal((B * S, latent)).astype(np.float32), prec)
+    scale = np.sqrt(1.0 / latent)
+    wk = seen((rng.standard_normal((latent, H * D)) * scale).astype(np.float32), prec)
+    wv = seen((rng.standard_normal((latent, H * D)) * scale).astype(np.float32), prec)
+    Q = seen(rng.standard_normal((B, H, S, D)).astype(np.float32), prec)
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=prec, causal=causal)
+    o = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
+    l = torch.empty((B, H, S), dtype=torch.float16, device=DEV)
+    dt = torch.float16 if prec == P.FP16 else torch.bfloat16
+    kb = torch.empty((B * S, H * D), dtype=dt, device=DEV)
+    vb = torch.empty((B * S, H * D), dtype=dt, device=DEV)
+    mfa.mla_forward(base, to_device(lat, prec), to_device(wk, prec), to_device(wv, prec),
+                    to_device(Q, prec), o, B, H, S, S, D, latent, prec, k_buf=kb, v_buf=vb,
+                    logsumexp=l)
+    torch.cuda.synchronize()
+    Kd = seen(ol.gemm(lat, wk), prec)
+    Vd = seen(ol.gemm(lat, wv), prec)
+    # [B*S, H*D] (BSHD) -> BHSD
+    to_bhsd = lambda x: np.ascontiguousarray(x.reshape(B, S, H, D).transpose(0, 2, 1, 3))
+    return o, l, kb, vb, Q, Kd, Vd, to_bhsd
+
+
+@pytest.mark.parametrize("prec", [P.FP16, P.BF16])
+@pytest.mark.parametrize("causal", [False, True])
+def test_mla_forward_small(gpu, prec, causal):
+    B, H, S, D, latent = 2, 4, 200, 64, 96
+    o, l, kb, vb, Q, Kd, Vd, to_bhsd = run_mla(B, H, S, D, latent, prec, causal)
+    tol = 2e-2 if prec == P.FP16 else 6e-2
+    assert relerr(kb, Kd) < tol and relerr(vb, Vd) < tol
+    ref = ol.attention(Q, to_bhsd(Kd), to_bhsd(Vd), causal=causal)
+    assert maxerr(o, ref["O"]) < (5e-2 if prec == P.FP16 else 1e-1)
+
+
+def test_mla_config4_one_head(gpu):
+    # BASELINE.json configs[3]: latent 512 -> D 128, bf16, S4096 (H16 assumed).
+    B, H, S, D, latent = 1, 16, 4096, 128, 512
+    o, l, kb, vb, Q, Kd, Vd, to_bhsd = run_mla(B, H, S, D, latent, P.BF16, seed=4)
+    assert relerr(kb, Kd) < 2e-2 and relerr(vb, Vd) < 2e-2
+    on = o.cpu().numpy()
+    assert np.isfinite(on).all()
+    h = 3
+    Kh = to_bhsd(kb.float().cpu().numpy())[:, h:h + 1]
+    Vh = to_bhsd(vb.float().cpu().numpy())[:, h:h + 1]
+    ref = ol.attention(Q[:, h:h + 1], Kh, Vh)
+    assert maxerr(on[:, h:h + 1], ref["O"]) < 2e-2

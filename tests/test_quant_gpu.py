@@ -1,0 +1,244 @@
+"""GPU parity for the INT8/INT4 path: runtime quantiser (bit-exact vs GEMMQuantization.swift's
+arithmetic), quantized forward/backward (QuantizedAttentionTest gates: INT8 relErr < 0.25,
+FP16 < 0.05, blockwise INT8 < 0.15; QuantizedAttentionTest.swift:441-791) and the
+dequant-exact property: with per-tensor scales the kernel's result equals attention on the
+dequantised K/V up to fp32 rounding."""
+import numpy as np
+import pytest
+import torch
+
+import mfa_amd as mfa
+import oracle_lib as ol
+from harness import maxerr, relerr, seen, to_device
+
+pytestmark = pytest.mark.gpu
+P = mfa.Precision
+DEV = "cuda:0"
+
+
+def tdev(x, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV).to(dtype)
+
+
+# ----------------------------------------------------------------------- quantiser
+@pytest.mark.parametrize("target", [P.INT8, P.INT4])
+@pytest.mark.parametrize("src", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(37, 19), (64, 128), (5, 1)])
+def test_runtime_quantize_tensorwise_bitexact(gpu, target, src, shape):
+    x = (np.random.default_rng(shape[0]).standard_normal(shape) * 3).astype(np.float32)
+    xt = tdev(x, src)
+    xs = xt.float().cpu().numpy()  # values after storage in `src`
+    data, scale, _, _ = mfa.quantize(xt, target, rows=shape[0], cols=shape[1])
+    torch.cuda.synchronize()
+    s_ref = ol.quant_scale_tensor(xs, int(target))
+    assert scale.item() == np.float32(s_ref)
+    q_ref = ol.quantize(xs, int(target), s_ref)
+    assert np.array_equal(data.cpu().numpy(), q_ref)
+
+
+@pytest.mark.parametrize("target", [P.INT8, P.INT4])
+@pytest.mark.parametrize("rows,cols,bs", [(16, 32, 8), (33, 20, 8), (128, 128, 64)])
+def test_runtime_quantize_blockwise_bitexact(gpu, target, rows, cols, bs):
+    rng = np.random.default_rng(rows + cols)
+    x = (rng.standard_normal((rows, cols)) * rng.random((rows, 1)) * 5).astype(np.float32)
+    data, _, bsc, bzp = mfa.quantize(tdev(x), target, mfa.QuantMode.blockwise, rows, cols, bs)
+    torch.cuda.synchronize()
+    s_ref = ol.quant_scales_block(x, rows, cols, bs, int(target))
+    assert np.array_equal(bsc.cpu().numpy(), s_ref)
+    assert not bzp.cpu().numpy().any()
+    assert np.array_equal(data.cpu().numpy(), ol.quantize_block(x, cols, bs, int(target), s_ref))
+
+
+def test_runtime_quantize_rowwise_scales(gpu):
+    x = np.random.default_rng(7).standard_normal((12, 33)).astype(np.float32)
+    data, _, sc, _ = mfa.quantize(tdev(x), P.INT8, mfa.QuantMode.rowWise, 12, 33)
+    torch.cuda.synchronize()
+    s_ref = ol.quant_scales_row(x, 12, 33, int(P.INT8))
+    assert np.array_equal(sc.cpu().numpy(), s_ref)
+    q = data.cpu().numpy().view(np.int8).reshape(12, 33)
+    for r in range(12):
+        assert np.array_equal(q[r], ol.quantize(x[r], int(P.INT8), s_ref[r]).view(np.int8))
+
+
+@pytest.mark.parametrize("target", [P.INT8, P.INT4])
+def test_dequantize_bitexact(gpu, target):
+    x = np.random.default_rng(11).standard_normal(1001).astype(np.float32)
+    s = ol.quant_scale_tensor(x, int(target))
+    q = ol.quantize(x, int(target), s)
+    t = mfa.quantized_tensor(tdev(q, torch.uint8), target, scale=s)
+    out = torch.empty(1001, dtype=torch.float32, device=DEV)
+    mfa.check(mfa.lib.mfa_dequantize(mfa.ctypes.byref(t), 1001, 1001, out.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ol.dequantize(q, 1001, int(target), s))
+
+
+# ----------------------------------------------------------------------- forward
+def quantize_host(x, prec):
+    s = ol.quant_scale_tensor(x, int(prec))
+    q = ol.quantize(x, int(prec), s)
+    return q, s, ol.dequantize(q, x.size, int(prec), s).reshape(x.shape)
+
+
+def run_qforward(Qn, Kn, Vn, qp, kp, vp, causal=False, lpi=True, blockwise=None):
+    B, H, R, D = Qn.shape
+    Hkv, C = Kn.shape[1], Kn.shape[2]
+    base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, low_precision_intermediates=lpi)
+    desc = mfa.quantized_descriptor(base, qp, kp, vp, B=B, H=H, Hkv=Hkv)
+    deq = {}
+
+    def make(x, prec, name):
+        if prec in (P.FP16, P.BF16, P.FP32):
+            xd = seen(x, prec)
+            deq[name] = xd
+            return mfa.quantized_tensor(to_device(x, prec), prec), None
+        if blockwise:
+            rows, cols = x.size // x.shape[-1], x.shape[-1]
+            sc = ol.quant_scales_block(x, rows, cols, blockwise, int(prec))
+            q = ol.quantize_block(x, cols, blockwise, int(prec), sc)
+            deq[name] = ol.dequantize_block(q, x.size, cols, blockwise, int(prec), sc).reshape(x.shape)
+            scd = tdev(sc)
+            return mfa.quantized_tensor(tdev(q, torch.uint8), prec, block_scales=scd,
+                                        block_size=blockwise), scd
+        q, s, d = quantize_host(x, prec)
+        deq[name] = d
+        return mfa.quantized_tensor(tdev(q, torch.uint8), prec, scale=s), None
+
+    tq, kq_keep = make(Qn, qp, "Q")
+    tk, kk_keep = make(Kn, kp, "K")
+    tv, kv_keep = make(Vn, vp, "V")
+    o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
+    l = torch.empty((B, H, R), dtype=torch.float16 if lpi else torch.float32, device=DEV)
+    mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+    torch.cuda.synchronize()
+    return o, l, deq, (kq_keep, kk_keep, kv_keep)
+
+
+@pytest.mark.parametrize("prec,gate", [(P.FP16, 0.05), (P.INT8, 0.25)])
+def test_quantized_forward_correctness_gate(gpu, prec, gate):
+    # QuantizedAttentionTest.testQuantizedForwardCorrectness: S32 D16, LCG 0x5EED5EED.
+    S, D = 32, 16
+    g = ol.LCGStream(0x5EED5EED)
+    Q, K, V = (g.draw(S * D).reshape(1, 1, S, D) for _ in range(3))
+    o, _, deq, _ = run_qforward(Q, K, V, prec, prec, prec, lpi=False)
+    ref = ol.attention(Q, K, V)["O"]
+    assert np.isfinite(o.cpu().numpy()).all()
+    assert relerr(o, ref) < gate
+    exact = ol.attention(deq["Q"], deq["K"], deq["V"])["O"]
+    assert maxerr(o, exact) < 5e-3  # dequant-exact: same math on the stored values
+
+
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("causal", [False, True])
+def test_quantized_forward_dequant_exact(gpu, kv, causal):
+    B, H, S, D = 2, 4, 200, 128
+    rng = np.random.default_rng(3)
+    Q, K, V = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
+    o, l, deq, _ = run_qforward(Q, K, V, P.FP16, kv, kv, causal=causal)
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"], causal=causal)
+    assert maxerr(o, ref["O"]) < 2e-2
+    assert maxerr(l, ref["L"]) < 1e-2
+    if kv == P.INT8:
+        assert relerr(o, ol.attention(Q, K, V, causal=causal)["O"]) < 0.25
+
+
+def test_blockwise_attention_forward_gate(gpu):
+    # QuantizedAttentionTest.testBlockwiseAttentionForward: S32 D32 bs8, gate 0.15.
+    S, D, bs = 32, 32, 8
+    i = np.arange(S * D)
+    br, bc = (i // D) // bs, (i % D) // bs
+    Q = ((i % 11).astype(np.float32) * np.float32(0.05) - np.float32(0.25)).reshape(1, 1, S, D)
+    K = (((i % 7).astype(np.float32) - 3) * ((br + 1) * (bc + 1)).astype(np.float32) * np.float32(0.1)).reshape(1, 1, S, D)
+    V = (((i % 5).astype(np.float32) - 2) * ((br + 1) * (bc + 1)).astype(np.float32) * np.float32(0.1)).reshape(1, 1, S, D)
+    o, _, deq, _ = run_qforward(Q, K, V, P.FP16, P.INT8, P.INT8, lpi=False, blockwise=bs)
+    assert relerr(o, ol.attention(Q, K, V)["O"]) < 0.15
+    assert maxerr(o, ol.attention(deq["Q"], deq["K"], deq["V"])["O"]) < 2e-3
+
+
+def test_int8_query_and_gqa(gpu):
+    B, H, Hkv, S, D = 1, 8, 2, 96, 64
+    rng = np.random.default_rng(4)
+    Q = rng.standard_normal((B, H, S, D)).astype(np.float32)
+    K, V = (rng.standard_normal((B, Hkv, S, D)).astype(np.float32) for _ in range(2))
+    o, _, deq, _ = run_qforward(Q, K, V, P.INT8, P.INT8, P.INT8)
+    assert maxerr(o, ol.attention(deq["Q"], deq["K"], deq["V"])["O"]) < 2e-2
+
+
+def test_c3_shape_one_head(gpu):
+    # BASELINE.json configs[2]: INT8 K/V, H16 S8192 D128; oracle on one head.
+    B, H, S, D = 1, 16, 8192, 128
+    n = B * H * S * D
+    Q = ol.lcg(11, n).reshape(B, H, S, D)
+    K = ol.lcg(22, n).reshape(B, H, S, D)
+    V = ol.lcg(33, n).reshape(B, H, S, D)
+    o, l, deq, _ = run_qforward(Q, K, V, P.FP16, P.INT8, P.INT8)
+    on = o.cpu().numpy()
+    assert np.isfinite(on).all() and np.abs(on).max() <= np.abs(deq["V"]).max() * 1.01
+    h = 5
+    ref = ol.attention(deq["Q"][:, h:h + 1], deq["K"][:, h:h + 1], deq["V"][:, h:h + 1])
+    assert maxerr(on[:, h:h + 1], ref["O"]) < 2e-3
+
+
+# ----------------------------------------------------------------------- backward
+@pytest.mark.parametrize("prec,gate", [(P.FP16, 0.05), (P.INT8, 0.25)])
+def test_quantized_backward_correctness_gate(gpu, prec, gate):
+    # QuantizedAttentionTest.testQuantizedBackwardCorrectness: S32 D16, LCG 0xBACC0DE; O and
+    # L (x log2 e) from the CPU reference; dO FP32; gates on dQ/dK/dV relative error.
+    S, D = 32, 16
+    g = ol.LCGStream(0xBACC0DE)
+    Q, K, V = (g.draw(S * D).reshape(1, 1, S, D) for _ in range(3))
+    dO = g.draw(S * D, 0.2, -0.1).reshape(1, 1, S, D)
+    ref = ol.attention(Q, K, V, dO=dO)
+    base = mfa.AttentionDescriptor.make(S, S, D)
+    desc = mfa.quantized_descriptor(base, prec, prec, prec)
+    keep = []
+
+    def make(x):
+        if prec == P.FP16:
+            return mfa.quantized_tensor(to_device(x, P.FP16), P.FP16)
+        q, s, _ = quantize_host(x, prec)
+        t = tdev(q, torch.uint8)
+        keep.append(t)
+        return mfa.quantized_tensor(t, prec, scale=s)
+
+    tq, tk, tv = make(Q), make(K), make(V)
+    o = tdev(ref["O"])
+    l = tdev(ref["L"])  # GPU convention (log2 units)
+    do = tdev(dO)
+    dq = torch.empty((1, 1, S, D), dtype=torch.float32, device=DEV)
+    dk, dv = torch.empty_like(dq), torch.empty_like(dq)
+    dvals = torch.empty((1, 1, S), dtype=torch.float32, device=DEV)
+    qa = mfa.QuantizedAttention()
+    qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
+    qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
+    torch.cuda.synchronize()
+    for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
+        assert np.isfinite(t.cpu().numpy()).all()
+        assert relerr(t, ref[name]) < gate, name
+
+
+def test_quantized_backward_dequant_exact(gpu):
+    B, H, S, D = 1, 2, 130, 64
+    rng = np.random.default_rng(8)
+    Q, K, V, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(4))
+    kq, ks, kd = quantize_host(K, P.INT8)
+    vq, vs, vd = quantize_host(V, P.INT8)
+    Qd = seen(Q, P.FP16)
+    ref = ol.attention(Qd, kd, vd, dO=dO, causal=True)
+    base = mfa.AttentionDescriptor.make(S, S, D, causal=True)
+    desc = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=B, H=H)
+    kt, vt = tdev(kq, torch.uint8), tdev(vq, torch.uint8)
+    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    tk = mfa.quantized_tensor(kt, P.INT8, scale=ks)
+    tv = mfa.quantized_tensor(vt, P.INT8, scale=vs)
+    o, l = tdev(ref["O"]), tdev(ref["L"])
+    do = tdev(dO)
+    dq = torch.empty((B, H, S, D), dtype=torch.float32, device=DEV)
+    dk, dv = torch.empty_like(dq), torch.empty_like(dq)
+    dvals = torch.empty((B, H, S), dtype=torch.float32, device=DEV)
+    qa = mfa.QuantizedAttention()
+    qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
+    qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
+    torch.cuda.synchronize()
+    assert maxerr(dvals, ref["D"]) < 1e-4
+    for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
+        assert maxerr(t, ref[name]) < 5e-2, name
