@@ -195,6 +195,33 @@ mfa_status_t plan_masks(const mfa_attention_descriptor_t& base, const void* mask
   return MFA_SUCCESS;
 }
 
+// The tuned forward kernel (attention_fwd_fast.hip) covers 16-bit operands with 16-byte aligned
+// rows (8-byte for INT8 K/V), D % 8 == 0, causal / window masks and per-tensor quantisation.
+bool fast_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
+  static const bool disabled = false;
+  (void)disabled;
+  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+    if (e[0] == '1') return false;
+  }
+  if (elem != 1 && elem != 2) return false;
+  if (kvsrc == 0 && DP != 64 && DP != 128) return false;
+  if (kvsrc == 1 && DP != 128) return false;
+  if (kvsrc > 1) return false;
+  if (p.D % 8 != 0 || p.mask.amask || p.mask.ranges) return false;
+  if (!p.q.vec || !p.k.vec || !p.v.vec) return false;
+  if (p.q.prec != (elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16)) return false;
+  if (p.k.bscale || p.v.bscale) return false;
+  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1;
+}
+
+hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, hipStream_t s) {
+  if (fast_eligible(p, elem, DP, kvsrc)) {
+    hipError_t e = mfa::fwd_fast_dispatch(p, elem, DP, kvsrc, s);
+    if (e != hipErrorNotSupported) return e;
+  }
+  return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
+}
+
 float resolve_scale(const mfa_attention_descriptor_t& d, int head_dim) {
   // AttentionKernel.swift:63-68: default 1/sqrt(head_dim).
   if (d.has_softmax_scale) return d.softmax_scale;
@@ -446,8 +473,7 @@ extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* 
   p.c_log2 = 1.442695041f * pl.scale;  // dotProductScale (AttentionKernel+Softmax.swift:17-25)
   p.o_mul = 1.f;
   p.mask = pl.mask;
-  return hip_status(mfa::fwd_dispatch(p, pl.elem, pl.DP, 0, 0, (hipStream_t)stream),
-                    "mfa_fwd launch");
+  return hip_status(launch_forward(p, pl.elem, pl.DP, 0, (hipStream_t)stream), "mfa_fwd launch");
 }
 
 // =========================================================================================
@@ -542,7 +568,7 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   p.o_mul = fv;
   if ((st = plan_masks(base, mask, R, C, &p.mask)) != MFA_SUCCESS) return st;
   if (R == 0) return MFA_SUCCESS;
-  return hip_status(mfa::fwd_dispatch(p, elem, DP, src_kind(kp), src_kind(vp), (hipStream_t)stream),
+  return hip_status(launch_forward(p, elem, DP, src_kind(kp), (hipStream_t)stream),
                     "mfa_fwd (quantized) launch");
 }
 
@@ -856,5 +882,5 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
   p.c_log2 = 1.442695041f * resolve_scale(desc->base, D);
   p.o_mul = 1.f;
   if ((st = plan_masks(desc->base, nullptr, Sq, Skv, &p.mask)) != MFA_SUCCESS) return st;
-  return hip_status(mfa::fwd_dispatch(p, elem, DP, 0, 0, s), "mfa_fwd (MLA) launch");
+  return hip_status(launch_forward(p, elem, DP, 0, s), "mfa_fwd (MLA) launch");
 }

@@ -48,6 +48,7 @@ hipError_t bwd_q_dispatch(const BwdParams& p, int elem, int DP, int ksrc, int vs
 hipError_t bwd_kv_dispatch(const BwdParams& p, int elem, int DP, int ksrc, int vsrc,
                            hipStream_t stream);
 int bwd_lds_bytes(int kind, int elem, int DP);
+hipError_t fwd_fast_dispatch(const FwdParams& p, int elem, int DP, int kvsrc, hipStream_t stream);
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream);
 
 }  // namespace mfa
