@@ -128,7 +128,8 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                      "peak": round(PEAK_FP16_TFLOPS, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": None,
-                     "kernel": "mfa_fwd_kernel<Arith16<F16,128>,128,64,4,0,0>",
+                     "kernel": ("mfa_fwd_pair_kernel<F16,128,64,SRC_SAME>" if S * H * B <= 768 * 128
+                                else "mfa_fwd_fast_kernel<F16,128,64,SRC_SAME>"),
                      "kernel_ms": round(kernel_ms, 4)},
     }
     del q, k, v, o, l
