@@ -292,7 +292,11 @@ typedef struct mfa_quantized_configuration {
   int32_t value_precision;  /* default INT8 */
   int32_t query_strategy, key_strategy, value_strategy;
   uint8_t strategy_version;
-  uint8_t reserved[3];
+  /* Extension (no reference counterpart): 1 = INT8 K/V run on the integer matrix cores
+   * (Q quantised per row in-kernel, P quantised to INT8; approximate).
+   * 0 (default) = dequantise-exact, the reference's FP32-multiply semantics. */
+  uint8_t integer_matmul;
+  uint8_t reserved[2];
   int32_t mixed_precision_intermediates;
 } mfa_quantized_configuration_t;
 

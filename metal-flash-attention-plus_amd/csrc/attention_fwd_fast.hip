@@ -167,6 +167,7 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
     const bool edge = t + BK > p.C;
     const bool diag = p.mask.causal && t + BK - 1 > q0;
     if (edge || diag || p.mask.window) {
+      MFA_KEEP_BRANCH();
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -402,6 +403,7 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
         const bool edge = t + BK > p.C;
         const bool diag = p.mask.causal && t + BK - 1 > q0;
         if (edge || diag || p.mask.window) {
+      MFA_KEEP_BRANCH();
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
 #pragma unroll

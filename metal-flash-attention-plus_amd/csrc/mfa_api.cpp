@@ -510,6 +510,24 @@ mfa_status_t quant_operand(const mfa_quantized_tensor_t* t, int cfg_prec, int B,
   return MFA_SUCCESS;
 }
 
+// The integer-matrix-core kernel (attention_fwd_i8.hip): FP16/BF16 Q, INT8 K/V with one
+// per-tensor scale and zero point 0, D % 16 == 0, D <= 128, no additive mask or sparse
+// ranges, dense rows.  Anything else runs the dequantise-exact path.
+bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
+  if (elem != 1 && elem != 2) return false;
+  if (is_quantized(qp) || kp != MFA_PRECISION_INT8 || vp != MFA_PRECISION_INT8) return false;
+  if (p.k.bscale || p.v.bscale || p.k.zp != 0 || p.v.zp != 0) return false;
+  if (p.D % 16 != 0 || p.D > 128 || p.mask.amask || p.mask.ranges) return false;
+  if (p.q.sd != 1 || p.k.sd != 1 || p.v.sd != 1) return false;
+  if (p.q.ss % 8 || p.q.sh % 8 || p.q.sb % 8) return false;
+  if (p.k.ss % 16 || p.k.sh % 16 || p.k.sb % 16) return false;
+  if (p.v.ss % 4 || p.v.sh % 4 || p.v.sb % 4) return false;
+  // Per-head K/V byte ranges are addressed with 32-bit buffer offsets.
+  if ((int64_t)p.C * p.k.ss >= (int64_t)1 << 31 || (int64_t)p.C * p.v.ss >= (int64_t)1 << 31) return false;
+  return ((uintptr_t)p.q.ptr % 16 == 0) && ((uintptr_t)p.k.ptr % 16 == 0) &&
+         ((uintptr_t)p.v.ptr % 4 == 0);
+}
+
 }  // namespace
 
 extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* desc,
@@ -568,6 +586,12 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   p.o_mul = fv;
   if ((st = plan_masks(base, mask, R, C, &p.mask)) != MFA_SUCCESS) return st;
   if (R == 0) return MFA_SUCCESS;
+  if (cfg.integer_matmul && i8mma_eligible(p, elem, qp, kp, vp)) {
+    mfa::FwdParams pi = p;
+    pi.nblk = (R + 127) / 128;
+    return hip_status(mfa::fwd_i8mma_dispatch(pi, elem, (hipStream_t)stream),
+                      "mfa_fwd (integer matmul) launch");
+  }
   return hip_status(launch_forward(p, elem, DP, src_kind(kp), (hipStream_t)stream),
                     "mfa_fwd (quantized) launch");
 }

@@ -208,10 +208,13 @@ struct Arith32 {
 // Rounded product that the compiler may not contract into a following add (hipcc's default
 // -ffp-contract=fast-honor-pragmas would otherwise fuse x*c - m into one FMA).
 __device__ __forceinline__ float mul_rn(float a, float b) {
-  float r;
-  asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
+#pragma clang fp contract(off)
+  return a * b;
 }
+
+// Keeps a rarely taken, wave-uniform branch (edge / diagonal tile masking) a branch: without
+// it the compiler if-converts the body into per-element selects that then run on every tile.
+#define MFA_KEEP_BRANCH() asm volatile("" ::: "memory")
 
 // Row index (within a 32-row MFMA output tile) of accumulator register i in lane half h.
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }

@@ -282,7 +282,8 @@ class QuantizedConfiguration(ctypes.Structure):
         ("key_strategy", ctypes.c_int32),
         ("value_strategy", ctypes.c_int32),
         ("strategy_version", ctypes.c_uint8),
-        ("reserved", ctypes.c_uint8 * 3),
+        ("integer_matmul", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 2),
         ("mixed_precision_intermediates", ctypes.c_int32),
     ]
 
@@ -469,13 +470,15 @@ def quantized_tensor(data, precision: Precision, scale=1.0, zero_point=0, block_
 
 
 def quantized_descriptor(base: AttentionDescriptor, q_prec=Precision.FP16, k_prec=Precision.INT8,
-                         v_prec=Precision.INT8, B=1, H=1, Hkv=None) -> QuantizedDescriptor:
+                         v_prec=Precision.INT8, B=1, H=1, Hkv=None,
+                         integer_matmul=False) -> QuantizedDescriptor:
     d = QuantizedDescriptor()
     d.base = base
     lib.mfa_quantized_configuration_init(ctypes.byref(d.config))
     d.config.query_precision = int(q_prec)
     d.config.key_precision = int(k_prec)
     d.config.value_precision = int(v_prec)
+    d.config.integer_matmul = 1 if integer_matmul else 0
     d.batch_size, d.num_heads = B, H
     d.num_kv_heads = H if Hkv is None else Hkv
     return d

@@ -79,11 +79,14 @@ def quantize_host(x, prec):
     return q, s, ol.dequantize(q, x.size, int(prec), s).reshape(x.shape)
 
 
-def run_qforward(Qn, Kn, Vn, qp, kp, vp, causal=False, lpi=True, blockwise=None):
+def run_qforward(Qn, Kn, Vn, qp, kp, vp, causal=False, lpi=True, blockwise=None,
+                 integer_matmul=False, window=None):
     B, H, R, D = Qn.shape
     Hkv, C = Kn.shape[1], Kn.shape[2]
-    base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, low_precision_intermediates=lpi)
-    desc = mfa.quantized_descriptor(base, qp, kp, vp, B=B, H=H, Hkv=Hkv)
+    base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, low_precision_intermediates=lpi,
+                                        window=window)
+    desc = mfa.quantized_descriptor(base, qp, kp, vp, B=B, H=H, Hkv=Hkv,
+                                    integer_matmul=integer_matmul)
     deq = {}
 
     def make(x, prec, name):
@@ -242,3 +245,57 @@ def test_quantized_backward_dequant_exact(gpu):
     assert maxerr(dvals, ref["D"]) < 1e-4
     for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
         assert maxerr(t, ref[name]) < 5e-2, name
+
+
+# ----------------------------------------------------------------------- integer matmul
+# The INT8-MFMA forward (attention_fwd_i8.hip) quantises Q per row and P to INT8, so it is not
+# dequant-exact.  Its tolerance, written here: relative L2 error vs attention on the
+# dequantised K/V (same stored values, float math) < 2.5e-2, max |L| error < 5e-2, and the
+# reference's own INT8 gate (relErr < 0.25 vs the unquantised inputs,
+# QuantizedAttentionTest.swift:519-520).
+I8MM_REL, I8MM_L = 2.5e-2, 5e-2
+
+
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,causal,window,qp", [
+    (2, 4, 4, 200, 200, 128, False, None, P.FP16),
+    (2, 4, 4, 200, 200, 128, True, None, P.FP16),
+    (1, 2, 2, 333, 333, 64, False, 40, P.FP16),
+    (1, 4, 2, 257, 129, 96, False, None, P.BF16),
+    (1, 2, 2, 512, 512, 128, False, 100, P.BF16),
+    (1, 1, 1, 1, 77, 16, False, None, P.FP16),
+    (1, 3, 1, 130, 1000, 128, False, None, P.FP16),
+])
+def test_integer_matmul_forward(gpu, B, H, Hkv, R, C, D, causal, window, qp):
+    rng = np.random.default_rng(R * 7 + C)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
+    o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8, causal=causal,
+                                integer_matmul=True, window=window)
+    on = o.cpu().numpy()
+    assert np.isfinite(on).all()
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"], causal=causal, window=window)
+    assert relerr(o, ref["O"]) < I8MM_REL
+    assert maxerr(l, ref["L"]) < I8MM_L
+    assert relerr(o, ol.attention(Q, K, V, causal=causal, window=window)["O"]) < 0.25
+
+
+def test_integer_matmul_ineligible_falls_back_exact(gpu):
+    # INT4 K/V (no integer-MFMA kernel) with integer_matmul set runs the dequant-exact path.
+    rng = np.random.default_rng(9)
+    Q, K, V = (rng.standard_normal((1, 2, 64, 64)).astype(np.float32) for _ in range(3))
+    o, _, deq, _ = run_qforward(Q, K, V, P.FP16, P.INT4, P.INT4, integer_matmul=True)
+    assert maxerr(o, ol.attention(deq["Q"], deq["K"], deq["V"])["O"]) < 2e-2
+
+
+def test_integer_matmul_c3_one_head(gpu):
+    B, H, S, D = 1, 16, 8192, 128
+    n = B * H * S * D
+    Q = ol.lcg(11, n).reshape(B, H, S, D)
+    K = ol.lcg(22, n).reshape(B, H, S, D)
+    V = ol.lcg(33, n).reshape(B, H, S, D)
+    o, l, deq, _ = run_qforward(Q, K, V, P.FP16, P.INT8, P.INT8, integer_matmul=True)
+    on = o.cpu().numpy()
+    assert np.isfinite(on).all()
+    h = 9
+    ref = ol.attention(deq["Q"][:, h:h + 1], deq["K"][:, h:h + 1], deq["V"][:, h:h + 1])
+    assert relerr(on[:, h:h + 1], ref["O"]) < I8MM_REL
