@@ -10,13 +10,13 @@
 //   * Q is quantised per row to INT8 in registers at kernel start (s_q = max|Q_row| / 127,
 //     round half away from zero, as GEMMQuantization.swift quantises);
 //   * S_int = Q_i8 · K_i8^T is exact in INT32; S = s_q · s_k · S_int;
-//   * softmax in FP32 as in the forward kernel, with the running max raised whenever it grows
-//     (so 0 <= P <= 1), then P_i8 = round(127 · P);
-//   * O_int += P_i8 · V_i8 exact in INT32 (rescaled by exp2(m_old - m_new) only when m moves);
-//     O = O_int · s_v / (127 · l), l = Σ P in FP32.
-// Layout: K tile [key][d] int8 (XOR-swizzled 16-byte chunks, row reads); V tile stored
-// transposed and key-permuted, V^T[d][pos(key)], so the A operand of O^T += V^T·P^T is one
-// 16-byte read and its k order matches the S accumulator registers that form P^T.
+//   * softmax in FP32 as in the forward kernel, with the running max raised (to an integer)
+//     whenever it grows, so 0 <= P <= 1; then P' = round(127 · P) as INT8;
+//   * O_int += P' · V_i8 exact in INT32 (rescaled by an exact power of two when m moves);
+//     O = O_int · s_v / l', l' = Σ 127·P in FP32.
+// Layout: K and V tiles [key][d] int8 in LDS (XOR-swizzled 16-byte chunks).  K is read by rows;
+// V through ds_read_b64_tr_b8, whose lanes pick the keys in the order of the S accumulator
+// registers, so P'^T feeds O^T += V^T·P'^T straight from registers.
 #include "mfa_stage.h"
 #include "mfa_dispatch.h"
 
@@ -36,16 +36,7 @@ __device__ __forceinline__ float xh_sum(float x) {
   return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
-// Position of key kk (0..31) of a 32-key sub-tile in the V^T image: accumulator register j of
-// lane half h holds key acc_row(j, h) = (j&3) + 8(j>>2) + 4h, stored at h*16 + j.
-__device__ __forceinline__ int key_pos(int kk) {
-  const int h = (kk >> 2) & 1;
-  const int j = (kk & 3) + 4 * (kk >> 3);
-  return h * 16 + j;
-}
-
-// [rows][64 bytes] image (V^T rows = head dim, 64 key positions): 4 chunks of 16 B per row.
-__device__ __forceinline__ int vt_off(int d, int chunk) { return d * 64 + 16 * (chunk ^ ((d >> 2) & 3)); }
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 template <class E, int DP, int BK>
 __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
@@ -55,7 +46,7 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   constexpr int NJ = BK / 32;
   constexpr int KSTEPS = DP / 32;       // i8 MFMA k = 32
   constexpr int KTILE = BK * DP;        // bytes
-  constexpr int VTILE = DP * BK;        // bytes
+  constexpr int VTILE = BK * DP;        // bytes
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const kb0 = smem;
   char* const vb0 = smem + 2 * KTILE;
@@ -126,13 +117,10 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   }
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
 
-  // ---- staging: K as 16-byte row chunks (2 per thread); V as 4 keys x 4 d byte blocks
-  // (2 per thread), transposed in registers and written to V^T[d][pos(key)].
+  // ---- staging: K and V as 16-byte row chunks, 2 of each per thread.
   const int8_t* kg = (const int8_t*)p.k.ptr + (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
   const int8_t* vg = (const int8_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
   constexpr int KCPR = DP / 16;  // 8 chunks per K row
-  uint4 rk[2];
-  uint32_t rv[2][4];
   // K/V arrive through buffer loads whose range check (num_records = the head's last byte)
   // returns 0 for rows past the end, so the tail tile needs no per-lane branches or clamps;
   // the per-thread offsets are fixed and the tile advances through soffset.  Columns past D
@@ -143,53 +131,49 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
       __builtin_amdgcn_make_buffer_rsrc((void*)kg, (short)0, (int)kbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t vrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)vg, (short)0, (int)vbytes, 0x00020000);
-  int koff[2], voff[2];
+  int koff[2], voff[2], lds_off[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int id = tid + i * NT;
     koff[i] = (id / KCPR) * (int)p.k.ss + (id % KCPR) * 16;
-    voff[i] = 4 * (id >> 5) * (int)p.v.ss + 4 * (id & 31);  // 4 keys x 4 d block
+    voff[i] = (id / KCPR) * (int)p.v.ss + (id % KCPR) * 16;
+    lds_off[i] = TK::off(id / KCPR, id % KCPR);
   }
-  const int vss = (int)p.v.ss;
+  uint4 rk[2], rv[2];
   auto load = [&](int t) {
-    const int ks = t * (int)p.k.ss, vs = t * vss;
+    const int ks = t * (int)p.k.ss, vs = t * (int)p.v.ss;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, koff[i], ks, 0);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, voff[i], vs, 0);
       rk[i] = make_uint4(a[0], a[1], a[2], a[3]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        rv[i][e] = __builtin_amdgcn_raw_buffer_load_b32(vrs, voff[i] + e * vss, vs, 0);
+      rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int id = tid + i * NT;
-      const int r = id / KCPR, cc = id % KCPR;
-      *reinterpret_cast<uint4*>(kb0 + buf * KTILE + TK::off(r, cc)) = rk[i];
-      const int kq = id >> 5, dq = id & 31;
-      // 4x4 byte transpose: rows e (keys) x bytes (d) -> words per d holding keys 0..3.
-      const uint32_t a = rv[i][0], bb = rv[i][1], c2 = rv[i][2], d2 = rv[i][3];
-      const uint32_t ab_lo = __builtin_amdgcn_perm(bb, a, 0x05010400u);  // a0 b0 a1 b1
-      const uint32_t ab_hi = __builtin_amdgcn_perm(bb, a, 0x07030602u);  // a2 b2 a3 b3
-      const uint32_t cd_lo = __builtin_amdgcn_perm(d2, c2, 0x05010400u);
-      const uint32_t cd_hi = __builtin_amdgcn_perm(d2, c2, 0x07030602u);
-      uint32_t u[4];
-      u[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);  // a0 b0 c0 d0
-      u[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);  // a1 b1 c1 d1
-      u[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
-      u[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
-      const int key0 = 4 * kq;               // 0..60, multiple of 4
-      const int js = key0 >> 5, kk = key0 & 31;
-      const int pos = js * 32 + key_pos(kk);  // 4 consecutive keys -> 4 consecutive positions
-      char* vt = vb0 + buf * VTILE;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int d = 4 * dq + e;
-        *reinterpret_cast<uint32_t*>(vt + vt_off(d, pos >> 4) + (pos & 15)) = u[e];
-      }
+      *reinterpret_cast<uint4*>(kb0 + buf * KTILE + lds_off[i]) = rk[i];
+      *reinterpret_cast<uint4*>(vb0 + buf * VTILE + lds_off[i]) = rv[i];
     }
+  };
+  // V^T operand via ds_read_b64_tr_b8: in each 16-lane group, lane 2j supplies the row of key
+  // acc_row(j + 8r, h) at column d0, lane 2j+1 the same row at d0 + 8; lane i < 8 receives
+  // column d0 + i of those 8 rows, lane 8 + i column d0 + 8 + i.
+  const int trj = (lane & 15) >> 1;
+  const int trg = (lane >> 4) & 1;
+  int tr_row[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) tr_row[r] = acc_row(trj + 8 * r, hh);
+  auto read_vt = [&](const char* vt, int j, int dt) -> i32x4 {
+    const int col = dt * 32 + 16 * trg + 8 * (lane & 1);
+    i32x2 v[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const char* pa = vt + TK::off(j * 32 + tr_row[r], col >> 4) + (col & 15);
+      v[r] = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)pa);
+    }
+    return i32x4{v[0][0], v[0][1], v[1][0], v[1][1]};
   };
 
   i32x16 oi[DP / 32];
@@ -249,16 +233,20 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sf[j][i]);
     const float m_tile = xh_max(mx) * cq;
+    // The running max is kept integer-valued (rounded up), so a rescale multiplies O_int by
+    // an exact power of two: one arithmetic shift per accumulator instead of a float round
+    // trip.  P' keeps at least 6 of its 7 bits (the rounded max exceeds the true one by < 1).
     if (__any(m_tile > m)) {
-      const float m_new = fmaxf(m, m_tile);
-      const float corr = __builtin_amdgcn_exp2f(m - m_new);
+      const float m_new = fmaxf(m, ceilf(m_tile));
+      const float dm = m_new - m;
+      lh *= __builtin_amdgcn_exp2f(-dm);
       m = m_new;
-      lh *= corr;
-      if (__any(corr != 1.f)) {
+      const int k = dm >= 31.f ? 32 : (int)dm;
+      if (__any(k != 0)) {
 #pragma unroll
         for (int dt = 0; dt < DP / 32; ++dt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) oi[dt][i] = (int)rintf((float)oi[dt][i] * corr);
+          for (int i = 0; i < 16; ++i) oi[dt][i] = k >= 32 ? 0 : (oi[dt][i] >> k);
       }
     }
     // P' = 127 P = exp2(s*c - (m - log2 127)) in [0, 127]; v_cvt_pk_u8_f32 rounds it into
@@ -293,8 +281,7 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
       // O^T += V^T · P'^T over this 32-key sub-tile (k order = accumulator registers).
 #pragma unroll
       for (int dt = 0; dt < DP / 32; ++dt) {
-        const i32x4 a = *reinterpret_cast<const i32x4*>(vt + vt_off(dt * 32 + l32, j * 2 + hh));
-        oi[dt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, pb, oi[dt], 0, 0, 0);
+        oi[dt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(read_vt(vt, j, dt), pb, oi[dt], 0, 0, 0);
       }
     }
     lh += rs;
