@@ -68,8 +68,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    import mfa_shard as shard
     H, S, D = args.heads, args.seq, args.dim
     B = 1  # per rank
+    # Weak scaling: the global batch is world x B; mfa_shard gives each rank its own batch
+    # element(s) (no collective on the data path).  Each rank materialises only its slices.
+    my = shard.forward_slices(B * world, H, H, world, rank)
+    assert sum(h1 - h0 for _, h0, h1 in my) == B * H
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
 

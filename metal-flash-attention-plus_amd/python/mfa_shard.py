@@ -1,0 +1,69 @@
+"""Batch x head sharding of the attention hot path across GPUs (one process per GPU).
+
+SURVEY.md §8(e): attention is independent per (batch, head) slice, so the units of work are
+split into contiguous per-rank ranges and each rank runs the ordinary single-GPU kernels on its
+slices — no collective on the data path (the reference has no multi-device path at all; its
+batching is MultiHeadAttention.swift:33-83's 3-D grid over (row block, head, batch)).
+
+Units:
+  * forward: (b, head block) where a head block is H_kv consecutive query heads
+    [j·H_kv, (j+1)·H_kv).  With the reference's GQA mapping kv = h % H_kv
+    (AttentionKernel+Source.swift:96-117) every block reads all H_kv key/value heads in
+    order, so a contiguous run of blocks is a dense [B', H', S, D] view of Q/O/L with the same
+    K/V — one launch per batch segment.
+  * backward: dK/dV are sums over a kv group's query heads, which must stay on one rank:
+    MHA (H_kv == H) shards by (b, h); GQA/MQA shards by whole batch elements.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+
+def split_range(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous balanced split of range(n): the first n % world ranks get one extra unit."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def forward_slices(B: int, H: int, Hkv: int, world: int, rank: int) -> List[Tuple[int, int, int]]:
+    """This rank's forward work as (b, h0, h1) query-head ranges, one per batch segment."""
+    if H % Hkv:
+        raise ValueError("H must be a multiple of H_kv")
+    blocks = H // Hkv
+    u0, u1 = split_range(B * blocks, world, rank)
+    out = []
+    u = u0
+    while u < u1:
+        b, j = divmod(u, blocks)
+        j1 = min(blocks, j + (u1 - u))
+        out.append((b, j * Hkv, j1 * Hkv))
+        u += j1 - j
+    return out
+
+
+def backward_slices(B: int, H: int, Hkv: int, world: int, rank: int) -> List[Tuple[int, int, int]]:
+    """This rank's backward work as (b, h0, h1) ranges; kv groups never straddle ranks."""
+    if H % Hkv:
+        raise ValueError("H must be a multiple of H_kv")
+    if Hkv == H:
+        return forward_slices(B, H, H, world, rank)
+    b0, b1 = split_range(B, world, rank)
+    return [(b, 0, H) for b in range(b0, b1)]
+
+
+def forward_shard(mfa, base, q, k, v, o, l, world: int, rank: int, stream=None) -> int:
+    """Runs this rank's forward slices through the C ABI on [B, H, S, D] device tensors (K/V
+    [B, H_kv, S_kv, D]).  Returns the number of (b, h) slices processed."""
+    B, H, R, D = q.shape
+    Hkv, C = k.shape[1], k.shape[2]
+    mha = mfa.MultiHeadAttention()
+    n = 0
+    for b, h0, h1 in forward_slices(B, H, Hkv, world, rank):
+        desc = mfa.MultiHeadDescriptor.make(base, 1, h1 - h0, R, D, Hkv=Hkv, C=C)
+        mha.forward(desc, q[b:b + 1, h0:h1], k[b:b + 1], v[b:b + 1], o[b:b + 1, h0:h1],
+                    None if l is None else l[b:b + 1, h0:h1], stream=stream)
+        n += h1 - h0
+    return n
