@@ -112,6 +112,10 @@ def main():
     value = total_flops / elapsed / 1e12
     achieved = flops_step / (kernel_ms * 1e-3) / 1e12
 
+    # The variant the library picks for this shape (mfa_api.cpp launch_forward: causal with
+    # <= 768 row blocks runs the mirrored-pair kernel).
+    kname = ("mfa_fwd_pair_kernel<F16, 128, 64, 0>" if (S + 127) // 128 * H * B <= 768
+             else "mfa_fwd_fast_kernel<F16, 128, 64, 0>")
     result = {
         "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
         "value": round(value, 2),
@@ -132,10 +136,9 @@ def main():
                    "gflop_per_step_per_gpu": round(flops_step / 1e9, 3)},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                      "peak": round(PEAK_FP16_TFLOPS, 1), "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": None,
-                     "kernel": ("mfa_fwd_pair_kernel<F16,128,64,SRC_SAME>" if S * H * B <= 768 * 128
-                                else "mfa_fwd_fast_kernel<F16,128,64,SRC_SAME>"),
-                     "kernel_ms": round(kernel_ms, 4)},
+                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
+                     "traffic": pmc_traffic(kname, S, H, D),
+                     "kernel": kname, "kernel_ms": round(kernel_ms, 4)},
     }
     del q, k, v, o, l
 
@@ -197,7 +200,7 @@ def main():
 
     # ---------------------------------------------------------------- CPU baseline
     if rank == 0 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(S, D)
+        result["cpu_baseline"] = cpu_baseline(S, D, H)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -205,25 +208,42 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(S: int, D: int):
-    """The CPU oracle (C restatement of Network.swift's naive reference) on ONE (batch, head)
-    slice of the headline workload, causal, all host threads (OpenMP over query rows)."""
+def pmc_traffic(kernel: str, S: int, H: int, D: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md), collected at the default bench shape only; None otherwise."""
+    if (S, H, D) != (4096, 16, 128):
+        return None
+    import glob
+    files = sorted(glob.glob(os.path.join(_REPO, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f).get(kernel)
+    return None if rec is None else round(rec["hbm_bytes"])
+
+
+def cpu_baseline(S: int, D: int, H: int):
+    """The CPU oracle (C restatement of Network.swift's naive reference) on the whole
+    headline workload (all H heads, causal), on the host's threads (OpenMP over query rows;
+    at most 16, the box's CPU share)."""
     sys.path.insert(0, os.path.join(_REPO, "tests"))
     import numpy as np
     import oracle_lib as ol
     threads = min(16, os.cpu_count() or 1)
     threads = ol.set_threads(threads)
     rng = np.random.default_rng(0)
-    q, k, v = ((rng.random((1, 1, S, D), dtype=np.float32) * 2 - 1) * 0.25 for _ in range(3))
+    q, k, v = ((rng.random((1, H, S, D), dtype=np.float32) * 2 - 1) * 0.25 for _ in range(3))
     t0 = time.perf_counter()
     ol.attention(q, k, v, causal=True)
     dt = time.perf_counter() - t0
-    flops = 4.0 * D * (S * (S + 1) // 2)
+    flops = 4.0 * D * (S * (S + 1) // 2) * H
     return {"value": round(flops / dt / 1e12, 5), "unit": "TFLOPS", "cores": threads,
             "kind": "port",
-            "sample": f"1 head of the headline workload (S={S}, D={D}, causal), "
-                      f"oracle/mfa_oracle.c forward, {dt:.2f}s; naive row-wise restatement "
-                      "of Network.swift (computes masked columns too, double accumulation)"}
+            "sample": f"the full headline workload (B=1, H={H}, S={S}, D={D}, causal, fp32 "
+                      f"inputs), oracle/mfa_oracle.c forward, {dt:.2f} s wall on {threads} "
+                      "threads; naive restatement of Network.swift (double accumulation; it "
+                      "computes the masked columns too, as the reference's CPU oracle does)"}
 
 
 if __name__ == "__main__":
