@@ -33,17 +33,164 @@ __device__ __forceinline__ float cross_half_sum(float x) {
   return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
+// K/V tile staging through range-checked buffer loads.  The descriptor is rebuilt per tile
+// from wave-uniform values (base advanced to the tile's first row, num_records = the bytes
+// left in the head), so rows past the end and chunks past D (offset forced out of range)
+// load as zeros without per-lane branches; the per-thread offsets are loop invariant.
+template <int DP, int BK, int NT, int KVSRC>
+struct KVStage {
+  using T = Tile16<DP>;
+  static constexpr int CPR = DP / 8;           // 8-element chunks per row
+  static constexpr int PER = BK * CPR / NT;    // chunks per thread per tile
+  static constexpr int RPI = NT / CPR;         // tile rows between a thread's chunks
+  static constexpr int ESZ = KVSRC == SRC_SAME ? 2 : 1;
+  static_assert(PER >= 1 && BK * CPR % NT == 0 && NT % CPR == 0, "tile/thread mismatch");
+  const char* kg;
+  const char* vg;
+  int kstep, vstep, kbytes, vbytes;
+  int koff, voff, loff;  // chunk 0's offsets; chunk i is RPI rows further (same swizzle)
+  uint4 rk[PER], rv[PER];
+
+  __device__ __forceinline__ void init(const FwdParams& p, int b, int kvh, int gt) {
+    kg = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * ESZ;
+    vg = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * ESZ;
+    kstep = (int)p.k.ss * ESZ;
+    vstep = (int)p.v.ss * ESZ;
+    kbytes = (int)(((int64_t)(p.C - 1) * p.k.ss + p.D) * ESZ);
+    vbytes = (int)(((int64_t)(p.C - 1) * p.v.ss + p.D) * ESZ);
+    const int row = gt / CPR, ch = gt % CPR;
+    const bool in = ch * 8 < p.D;
+    koff = in ? row * kstep + ch * 8 * ESZ : 0x40000000;
+    voff = in ? row * vstep + ch * 8 * ESZ : 0x40000000;
+    loff = T::off(row, ch);
+  }
+  __device__ __forceinline__ void load(int t) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int kb = (t + i * RPI) * kstep, vb = (t + i * RPI) * vstep;
+      const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(kg + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
+      const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(vg + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
+      if constexpr (KVSRC == SRC_SAME) {
+        const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, koff, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0);
+        rk[i] = make_uint4(a[0], a[1], a[2], a[3]);
+        rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      } else {  // INT8: 8 bytes per chunk
+        const auto a = __builtin_amdgcn_raw_buffer_load_b64(krs, koff, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(vrs, voff, 0, 0);
+        rk[i] = make_uint4(a[0], a[1], 0u, 0u);
+        rv[i] = make_uint4(v[0], v[1], 0u, 0u);
+      }
+    }
+  }
+  template <class E>
+  __device__ __forceinline__ void store(char* kt, char* vt, float kzp, float vzp) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      uint4 a = rk[i], v = rv[i];
+      if constexpr (KVSRC != SRC_SAME) {
+        a = dequant_fast<E, KVSRC>(a, kzp);
+        v = dequant_fast<E, KVSRC>(v, vzp);
+      }
+      *reinterpret_cast<uint4*>(kt + loff + i * RPI * T::ROWB) = a;
+      *reinterpret_cast<uint4*>(vt + loff + i * RPI * T::ROWB) = v;
+    }
+  }
+};
+
+// One 64-key tile of the forward for one wave (32 query rows): S^T = K·Q^T, masks, online
+// softmax (lazy rescale), O^T += V^T·P^T.  Shared by the single-block and pair kernels.
+template <class E, int DP, int BK>
+__device__ __forceinline__ void fwd_tile(const char* kt, const char* vt,
+                                         const i16x8 (&qf)[DP / 16], f32x16 (&o)[DP / 32],
+                                         float& m, float& lh, int t, int q0, int qi,
+                                         const FwdParams& p, float c, int wsz, int lane) {
+  using A = Arith16<E, DP>;
+  constexpr int NJ = BK / 32;
+  constexpr float THR = 8.0f;  // lazy-rescale threshold (log2 units)
+  const int l32 = lane & 31, hh = lane >> 5;
+  f32x16 s[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) s[j] = zero16();
+#pragma unroll
+  for (int ds = 0; ds < A::DSTEPS; ++ds)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      s[j] = A::mma(A::read_row(kt, j * 32 + l32, ds, hh), qf[ds], s[j]);
+
+  // Masks: only tiles that reach past the diagonal / edge / window.
+  const bool edge = t + BK > p.C;
+  const bool diag = p.mask.causal && t + BK - 1 > q0;
+  if (edge || diag || p.mask.window) {
+    MFA_KEEP_BRANCH();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = t + j * 32 + acc_row(i, hh);
+        float x = s[j][i];
+        if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) x = kMaskValue;
+        if (key >= p.C) x = -__builtin_inff();
+        s[j][i] = x;
+      }
+  }
+
+  float mx = s[0][0];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[j][i]);
+  const float m_tile = cross_half_max(mx) * c;
+  if (__any(m_tile > m + THR)) {
+    const float m_new = fmaxf(m, m_tile);
+    const float corr = __builtin_amdgcn_exp2f(m - m_new);
+    m = m_new;
+    lh *= corr;
+#pragma unroll
+    for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[dt][i] *= corr;
+  }
+  // P = exp2(s·c − m); four independent partial row sums keep the adds off one serial chain.
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (__any(m < kMaskLevel)) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = __builtin_amdgcn_exp2f(mul_rn(s[j][i], c) - m);
+        s[j][i] = pv;
+        rs[i & 3] += pv;
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -m));
+        s[j][i] = pv;
+        rs[i & 3] += pv;
+      }
+  }
+  lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
+
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const i16x8 pb = A::pack(s[j], ks);
+#pragma unroll
+      for (int dt = 0; dt < DP / 32; ++dt)
+        o[dt] = A::mma(A::read_tr(vt, j * 32, ks, dt * 32, lane), pb, o[dt]);
+    }
+}
+
 template <class E, int DP, int BK, int KVSRC>
 __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
-  using A = Arith16<E, DP>;
-  using T = Tile16<DP>;
-  constexpr int NW = 4, NT = 256, BQ = 128;
-  constexpr int NJ = BK / 32;
+  constexpr int NT = 256, BQ = 128;
   constexpr int TILEB = BK * DP * 2;
-  constexpr int CPR = DP / 8;                 // 16-byte chunks per row
-  constexpr int PER = BK * CPR / NT;          // chunks per thread per tile
-  static_assert(PER >= 1 && BK * CPR % NT == 0, "tile/thread mismatch");
-  constexpr float THR = 8.0f;                 // lazy-rescale threshold (log2 units)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const kb0 = smem;
   char* const vb0 = smem + 2 * TILEB;
@@ -60,16 +207,16 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
   const int qi = q0 + wave * 32 + l32;
   const bool qvalid = qi < p.R;
 
-  typename A::frag qf[A::DSTEPS];
-  {
-    const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh +
-                           (int64_t)(qvalid ? qi : 0) * p.q.ss;
+  i16x8 qf[DP / 16];
 #pragma unroll
-    for (int s = 0; s < A::DSTEPS; ++s) {
+  for (int s = 0; s < DP / 16; ++s) qf[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  {
+    const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb +
+                           (int64_t)h * p.q.sh + (int64_t)(qvalid ? qi : 0) * p.q.ss;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
       const int d0 = 16 * s + 8 * hh;
-      i16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (qvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-      qf[s] = v;
+      if (qvalid && d0 < p.D) qf[s] = *reinterpret_cast<const i16x8*>(qrow + d0);
     }
   }
 
@@ -81,58 +228,9 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
     kbeg = lo > 0 ? (int)(lo / BK) * BK : 0;
   }
 
-  // Staging geometry: chunk id = tid + i*NT -> (row, chunk) of the tile; loop invariant.
-  const int esz = KVSRC == SRC_SAME ? 2 : 1;  // bytes per stored element
-  const int64_t kbase = (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
-  const int64_t vbase = (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
-  const char* kg = (const char*)p.k.ptr + kbase * esz;
-  const char* vg = (const char*)p.v.ptr + vbase * esz;
-  int srow[PER], soff[PER];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int id = tid + i * NT;
-    srow[i] = id / CPR;
-    soff[i] = T::off(id / CPR, id % CPR);
-  }
-  uint4 rk[PER], rv[PER];
-  auto load = [&](int t) {
-    const bool full = t + BK <= p.C;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int id = tid + i * NT;
-      const int64_t row = t + srow[i];
-      const int c = id % CPR;
-      uint4 a = make_uint4(0u, 0u, 0u, 0u), v = a;
-      if (full || row < p.C) {
-        if constexpr (KVSRC == SRC_SAME) {
-          if (c * 8 < p.D) {
-            a = *reinterpret_cast<const uint4*>(kg + (row * p.k.ss + c * 8) * 2);
-            v = *reinterpret_cast<const uint4*>(vg + (row * p.v.ss + c * 8) * 2);
-          }
-        } else {  // INT8: 8 bytes per chunk
-          if (c * 8 < p.D) {
-            const uint2 ka = *reinterpret_cast<const uint2*>(kg + row * p.k.ss + c * 8);
-            const uint2 va = *reinterpret_cast<const uint2*>(vg + row * p.v.ss + c * 8);
-            a.x = ka.x; a.y = ka.y; v.x = va.x; v.y = va.y;
-          }
-        }
-      }
-      rk[i] = a;
-      rv[i] = v;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      uint4 a = rk[i], v = rv[i];
-      if constexpr (KVSRC != SRC_SAME) {
-        a = dequant_fast<E, KVSRC>(a, (float)p.k.zp);
-        v = dequant_fast<E, KVSRC>(v, (float)p.v.zp);
-      }
-      *reinterpret_cast<uint4*>(kb0 + buf * TILEB + soff[i]) = a;
-      *reinterpret_cast<uint4*>(vb0 + buf * TILEB + soff[i]) = v;
-    }
-  };
+  KVStage<DP, BK, NT, KVSRC> st;
+  st.init(p, b, kvh, tid);
+  const float kzp = (float)p.k.zp, vzp = (float)p.v.zp;
 
   f32x16 o[DP / 32];
 #pragma unroll
@@ -142,93 +240,18 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
 
   if (kbeg < kend) {
-    load(kbeg);
-    store(0);
+    st.load(kbeg);
+    st.template store<E>(kb0, vb0, kzp, vzp);
   }
   __syncthreads();
 
   int cur = 0;
   for (int t = kbeg; t < kend; t += BK) {
     const bool has_next = t + BK < kend;
-    if (has_next) load(t + BK);
-    const char* kt = kb0 + cur * TILEB;
-    const char* vt = vb0 + cur * TILEB;
-
-    f32x16 s[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) s[j] = zero16();
-#pragma unroll
-    for (int ds = 0; ds < A::DSTEPS; ++ds)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        s[j] = A::mma(A::read_row(kt, j * 32 + l32, ds, hh), qf[ds], s[j]);
-
-    // Masks: only tiles that reach past the diagonal / edge / window.
-    const bool edge = t + BK > p.C;
-    const bool diag = p.mask.causal && t + BK - 1 > q0;
-    if (edge || diag || p.mask.window) {
-      MFA_KEEP_BRANCH();
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = t + j * 32 + acc_row(i, hh);
-          float x = s[j][i];
-          if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) x = kMaskValue;
-          if (key >= p.C) x = -__builtin_inff();
-          s[j][i] = x;
-        }
-    }
-
-    float mx = s[0][0];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[j][i]);
-    const float m_tile = cross_half_max(mx) * c;
-    if (__any(m_tile > m + THR)) {
-      const float m_new = fmaxf(m, m_tile);
-      const float corr = __builtin_amdgcn_exp2f(m - m_new);
-      m = m_new;
-      lh *= corr;
-#pragma unroll
-      for (int dt = 0; dt < DP / 32; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= corr;
-    }
-    float rs = 0.f;
-    if (__any(m < kMaskLevel)) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float pv = __builtin_amdgcn_exp2f(mul_rn(s[j][i], c) - m);
-          s[j][i] = pv;
-          rs += pv;
-        }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float pv = __builtin_amdgcn_exp2f(s[j][i] * c - m);
-          s[j][i] = pv;
-          rs += pv;
-        }
-    }
-    lh += rs;
-
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const i16x8 pb = A::pack(s[j], ks);
-#pragma unroll
-        for (int dt = 0; dt < DP / 32; ++dt)
-          o[dt] = A::mma(A::read_tr(vt, j * 32, ks, dt * 32, lane), pb, o[dt]);
-      }
-
-    if (has_next) store(cur ^ 1);
+    if (has_next) st.load(t + BK);
+    fwd_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, qf, o, m, lh, t, q0, qi, p, c,
+                        wsz, lane);
+    if (has_next) st.template store<E>(kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB, kzp, vzp);
     __syncthreads();
     cur ^= 1;
   }
@@ -269,19 +292,14 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
 // each), group 1 idling through the odd step.
 template <class E, int DP, int BK, int KVSRC>
 __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
-  using A = Arith16<E, DP>;
-  using T = Tile16<DP>;
   constexpr int NT = 256, BQ = 128;
-  constexpr int NJ = BK / 32;
   constexpr int TILEB = BK * DP * 2;
-  constexpr int CPR = DP / 8;
-  constexpr int PER = BK * CPR / NT;
-  static_assert(PER >= 1 && BK * CPR % NT == 0, "tile/thread mismatch");
-  constexpr float THR = 8.0f;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
-  const int g = tid >> 8;             // group
+  // Group index, wave-uniform; readfirstlane makes that provable, so the per-tile buffer
+  // descriptors (built from t, which depends on g) stay in SGPRs without waterfall loops.
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
   const int gt = tid & 255;           // thread within group
   const int lane = tid & 63, wg = gt >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -296,51 +314,9 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
   const float c = p.c_log2;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
 
-  const int esz = KVSRC == SRC_SAME ? 2 : 1;
-  const char* kg = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * esz;
-  const char* vg = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * esz;
-  int srow[PER], soff[PER];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int id = gt + i * NT;
-    srow[i] = id / CPR;
-    soff[i] = T::off(id / CPR, id % CPR);
-  }
-  uint4 rk[PER], rv[PER];
-  auto load = [&](int t) {
-    const bool full = t + BK <= p.C;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int id = gt + i * NT;
-      const int64_t row = t + srow[i];
-      const int cc = id % CPR;
-      uint4 a = make_uint4(0u, 0u, 0u, 0u), v = a;
-      if ((full || row < p.C) && cc * 8 < p.D) {
-        if constexpr (KVSRC == SRC_SAME) {
-          a = *reinterpret_cast<const uint4*>(kg + (row * p.k.ss + cc * 8) * 2);
-          v = *reinterpret_cast<const uint4*>(vg + (row * p.v.ss + cc * 8) * 2);
-        } else {
-          const uint2 ka = *reinterpret_cast<const uint2*>(kg + row * p.k.ss + cc * 8);
-          const uint2 va = *reinterpret_cast<const uint2*>(vg + row * p.v.ss + cc * 8);
-          a.x = ka.x; a.y = ka.y; v.x = va.x; v.y = va.y;
-        }
-      }
-      rk[i] = a;
-      rv[i] = v;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      uint4 a = rk[i], v = rv[i];
-      if constexpr (KVSRC != SRC_SAME) {
-        a = dequant_fast<E, KVSRC>(a, (float)p.k.zp);
-        v = dequant_fast<E, KVSRC>(v, (float)p.v.zp);
-      }
-      *reinterpret_cast<uint4*>(kb0 + buf * TILEB + soff[i]) = a;
-      *reinterpret_cast<uint4*>(vb0 + buf * TILEB + soff[i]) = v;
-    }
-  };
+  KVStage<DP, BK, NT, KVSRC> st;
+  st.init(p, b, kvh, gt);
+  const float kzp = (float)p.k.zp, vzp = (float)p.v.zp;
 
   const int rbA = pi, rbB = p.nblk - 1 - pi;
   for (int which = 0; which < 2; ++which) {
@@ -350,16 +326,16 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
     const int qi = q0 + wg * 32 + l32;
     const bool qvalid = qi < p.R;
 
-    i16x8 qf[A::DSTEPS];
+    i16x8 qf[DP / 16];
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) qf[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
     {
       const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb +
                              (int64_t)h * p.q.sh + (int64_t)(qvalid ? qi : 0) * p.q.ss;
 #pragma unroll
-      for (int s = 0; s < A::DSTEPS; ++s) {
+      for (int s = 0; s < DP / 16; ++s) {
         const int d0 = 16 * s + 8 * hh;
-        i16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (qvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-        qf[s] = v;
+        if (qvalid && d0 < p.D) qf[s] = *reinterpret_cast<const i16x8*>(qrow + d0);
       }
     }
     int kend = p.C;
@@ -380,8 +356,8 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
     float m = -kFltMax, lh = 0.f;
 
     if (t0 < t1) {
-      load(t0);
-      store(0);
+      st.load(t0);
+      st.template store<E>(kb0, vb0, kzp, vzp);
     }
     __syncthreads();
     int cur = 0;
@@ -389,79 +365,11 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
       const int t = t0 + step * BK;
       if (t < t1) {
         const bool has_next = t + BK < t1;
-        if (has_next) load(t + BK);
-        const char* kt = kb0 + cur * TILEB;
-        const char* vt = vb0 + cur * TILEB;
-        f32x16 s[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) s[j] = zero16();
-#pragma unroll
-        for (int ds = 0; ds < A::DSTEPS; ++ds)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            s[j] = A::mma(A::read_row(kt, j * 32 + l32, ds, hh), qf[ds], s[j]);
-        const bool edge = t + BK > p.C;
-        const bool diag = p.mask.causal && t + BK - 1 > q0;
-        if (edge || diag || p.mask.window) {
-      MFA_KEEP_BRANCH();
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int key = t + j * 32 + acc_row(i, hh);
-              float x = s[j][i];
-              if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) x = kMaskValue;
-              if (key >= p.C) x = -__builtin_inff();
-              s[j][i] = x;
-            }
-        }
-        float mx = s[0][0];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[j][i]);
-        const float m_tile = cross_half_max(mx) * c;
-        if (__any(m_tile > m + THR)) {
-          const float m_new = fmaxf(m, m_tile);
-          const float corr = __builtin_amdgcn_exp2f(m - m_new);
-          m = m_new;
-          lh *= corr;
-#pragma unroll
-          for (int dt = 0; dt < DP / 32; ++dt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[dt][i] *= corr;
-        }
-        float rs = 0.f;
-        if (__any(m < kMaskLevel)) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const float pv = __builtin_amdgcn_exp2f(mul_rn(s[j][i], c) - m);
-              s[j][i] = pv;
-              rs += pv;
-            }
-        } else {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const float pv = __builtin_amdgcn_exp2f(s[j][i] * c - m);
-              s[j][i] = pv;
-              rs += pv;
-            }
-        }
-        lh += rs;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const i16x8 pb = A::pack(s[j], ks);
-#pragma unroll
-            for (int dt = 0; dt < DP / 32; ++dt)
-              o[dt] = A::mma(A::read_tr(vt, j * 32, ks, dt * 32, lane), pb, o[dt]);
-          }
-        if (has_next) store(cur ^ 1);
+        if (has_next) st.load(t + BK);
+        fwd_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, qf, o, m, lh, t, q0, qi, p,
+                            c, wsz, lane);
+        if (has_next)
+          st.template store<E>(kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB, kzp, vzp);
       }
       __syncthreads();
       cur ^= 1;

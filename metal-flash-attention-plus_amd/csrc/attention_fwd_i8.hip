@@ -121,31 +121,29 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   const int8_t* kg = (const int8_t*)p.k.ptr + (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
   const int8_t* vg = (const int8_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
   constexpr int KCPR = DP / 16;  // 8 chunks per K row
-  // K/V arrive through buffer loads whose range check (num_records = the head's last byte)
-  // returns 0 for rows past the end, so the tail tile needs no per-lane branches or clamps;
-  // the per-thread offsets are fixed and the tile advances through soffset.  Columns past D
-  // in a row read the next row's bytes: Q is zero there and O columns >= D are not stored.
-  const uint32_t kbytes = (uint32_t)((int64_t)(p.C - 1) * p.k.ss + p.D);
-  const uint32_t vbytes = (uint32_t)((int64_t)(p.C - 1) * p.v.ss + p.D);
-  const __amdgpu_buffer_rsrc_t krs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)kg, (short)0, (int)kbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t vrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)vg, (short)0, (int)vbytes, 0x00020000);
-  int koff[2], voff[2], lds_off[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int id = tid + i * NT;
-    koff[i] = (id / KCPR) * (int)p.k.ss + (id % KCPR) * 16;
-    voff[i] = (id / KCPR) * (int)p.v.ss + (id % KCPR) * 16;
-    lds_off[i] = TK::off(id / KCPR, id % KCPR);
-  }
+  // K/V arrive through buffer loads whose range check returns 0 past the head's last byte: the
+  // descriptor is rebuilt per tile from wave-uniform values (base at the tile's rows,
+  // num_records = bytes left), so the tail tile needs no per-lane branches or clamps.  Columns
+  // past D in a row read the next row's bytes: Q is zero there and O columns >= D are not
+  // stored.
+  const int kbytes = (int)((int64_t)(p.C - 1) * p.k.ss + p.D);
+  const int vbytes = (int)((int64_t)(p.C - 1) * p.v.ss + p.D);
+  const int kss = (int)p.k.ss, vss = (int)p.v.ss;
+  constexpr int RPI = NT / KCPR;  // rows between a thread's two chunks
+  const int koff = (tid / KCPR) * kss + (tid % KCPR) * 16;
+  const int voff = (tid / KCPR) * vss + (tid % KCPR) * 16;
+  const int lds_off = TK::off(tid / KCPR, tid % KCPR);  // chunk 1: +RPI rows, same swizzle
   uint4 rk[2], rv[2];
   auto load = [&](int t) {
-    const int ks = t * (int)p.k.ss, vs = t * (int)p.v.ss;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, koff[i], ks, 0);
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, voff[i], vs, 0);
+      const int kb = (t + i * RPI) * kss, vb = (t + i * RPI) * vss;
+      const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(kg + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
+      const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(vg + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, koff, 0, 0);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0);
       rk[i] = make_uint4(a[0], a[1], a[2], a[3]);
       rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
@@ -153,8 +151,8 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(kb0 + buf * KTILE + lds_off[i]) = rk[i];
-      *reinterpret_cast<uint4*>(vb0 + buf * VTILE + lds_off[i]) = rv[i];
+      *reinterpret_cast<uint4*>(kb0 + buf * KTILE + lds_off + i * RPI * TK::ROWB) = rk[i];
+      *reinterpret_cast<uint4*>(vb0 + buf * VTILE + lds_off + i * RPI * TK::ROWB) = rv[i];
     }
   };
   // V^T operand via ds_read_b64_tr_b8: in each 16-lane group, lane 2j supplies the row of key

@@ -211,6 +211,11 @@ bool fast_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
   if (!p.q.vec || !p.k.vec || !p.v.vec) return false;
   if (p.q.prec != (elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16)) return false;
   if (p.k.bscale || p.v.bscale) return false;
+  // K/V are addressed per head with 32-bit buffer offsets (attention_fwd_fast.hip KVStage).
+  const int64_t esz = kvsrc == 0 ? 2 : 1;
+  if ((int64_t)p.C * p.k.ss * esz >= ((int64_t)1 << 31) ||
+      (int64_t)p.C * p.v.ss * esz >= ((int64_t)1 << 31))
+    return false;
   return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1;
 }
 
