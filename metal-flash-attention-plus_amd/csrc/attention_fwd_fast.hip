@@ -39,11 +39,12 @@ __device__ __forceinline__ float cross_half_sum(float x) {
 // load as zeros without per-lane branches; the per-thread offsets are loop invariant.
 template <int DP, int BK, int NT, int KVSRC>
 struct KVStage {
+  // INT8 K/V (dequantised on the way into LDS): register staging through buffer loads.
   using T = Tile16<DP>;
   static constexpr int CPR = DP / 8;           // 8-element chunks per row
   static constexpr int PER = BK * CPR / NT;    // chunks per thread per tile
   static constexpr int RPI = NT / CPR;         // tile rows between a thread's chunks
-  static constexpr int ESZ = KVSRC == SRC_SAME ? 2 : 1;
+  static constexpr int ESZ = 1;
   static_assert(PER >= 1 && BK * CPR % NT == 0 && NT % CPR == 0, "tile/thread mismatch");
   const char* kg;
   const char* vg;
@@ -72,33 +73,81 @@ struct KVStage {
           (void*)(kg + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
       const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(vg + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
-      if constexpr (KVSRC == SRC_SAME) {
-        const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, koff, 0, 0);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0);
-        rk[i] = make_uint4(a[0], a[1], a[2], a[3]);
-        rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
-      } else {  // INT8: 8 bytes per chunk
-        const auto a = __builtin_amdgcn_raw_buffer_load_b64(krs, koff, 0, 0);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(vrs, voff, 0, 0);
-        rk[i] = make_uint4(a[0], a[1], 0u, 0u);
-        rv[i] = make_uint4(v[0], v[1], 0u, 0u);
-      }
+      const auto a = __builtin_amdgcn_raw_buffer_load_b64(krs, koff, 0, 0);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(vrs, voff, 0, 0);
+      rk[i] = make_uint4(a[0], a[1], 0u, 0u);
+      rv[i] = make_uint4(v[0], v[1], 0u, 0u);
     }
   }
   template <class E>
   __device__ __forceinline__ void store(char* kt, char* vt, float kzp, float vzp) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      uint4 a = rk[i], v = rv[i];
-      if constexpr (KVSRC != SRC_SAME) {
-        a = dequant_fast<E, KVSRC>(a, kzp);
-        v = dequant_fast<E, KVSRC>(v, vzp);
-      }
-      *reinterpret_cast<uint4*>(kt + loff + i * RPI * T::ROWB) = a;
-      *reinterpret_cast<uint4*>(vt + loff + i * RPI * T::ROWB) = v;
+      *reinterpret_cast<uint4*>(kt + loff + i * RPI * T::ROWB) = dequant_fast<E, KVSRC>(rk[i], kzp);
+      *reinterpret_cast<uint4*>(vt + loff + i * RPI * T::ROWB) = dequant_fast<E, KVSRC>(rv[i], vzp);
     }
   }
 };
+
+// 16-bit K/V: LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave-instruction) straight
+// into the XOR-swizzled tile, no staging registers and no ds_write.  A piece covers RP rows;
+// lane l lands at byte 16*l of it (row n*RP + l/CPR, physical chunk l%CPR) and so fetches
+// the logical chunk (l%CPR) ^ swz(row).  Wave w of the NW staging waves issues pieces
+// n = w + NW*i, and swz depends only on row & 15, so each wave needs one lane offset per
+// tensor.  Rows past the end and chunks past D read as zeros (range-checked descriptor built
+// per piece from wave-uniform values).
+template <int DP, int BK, int NT>
+struct KVStage<DP, BK, NT, SRC_SAME> {
+  using T = Tile16<DP>;
+  static constexpr int NW = NT / 64;
+  static constexpr int CPR = DP / 8;
+  static constexpr int RP = 1024 / T::ROWB;           // rows per piece
+  static constexpr int NPIECE = BK / RP;              // pieces per tile
+  static constexpr int PPW = NPIECE / NW;             // pieces per wave
+  static_assert(NPIECE % NW == 0 && (16 % RP == 0 || RP % 16 == 0), "DMA geometry");
+  static_assert((NW * RP) % 16 == 0, "one swizzle phase per wave");
+  const char* kg;
+  const char* vg;
+  int kstep, vstep, kbytes, vbytes;
+  int koff, voff, w;
+
+  __device__ __forceinline__ void init(const FwdParams& p, int b, int kvh, int gt) {
+    kg = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
+    vg = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
+    kstep = (int)p.k.ss * 2;
+    vstep = (int)p.v.ss * 2;
+    kbytes = (int)(((int64_t)(p.C - 1) * p.k.ss + p.D) * 2);
+    vbytes = (int)(((int64_t)(p.C - 1) * p.v.ss + p.D) * 2);
+    w = __builtin_amdgcn_readfirstlane(gt >> 6);
+    const int l = gt & 63;
+    const int rl = l / CPR, pc = l % CPR;
+    const int row = w * RP + rl;                       // row of this wave's first piece
+    const int ch = pc ^ T::swz(row);
+    const bool in = ch * 8 < p.D;
+    koff = in ? rl * kstep + ch * 16 : 0x40000000;
+    voff = in ? rl * vstep + ch * 16 : 0x40000000;
+  }
+  __device__ __forceinline__ void issue(int t, char* kt, char* vt) const {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int n = w + NW * i;
+      const int kb = (t + n * RP) * kstep, vb = (t + n * RP) * vstep;
+      const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(kg + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
+      const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(vg + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          krs, (__attribute__((address_space(3))) void*)(kt + n * 1024), 16, koff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          vrs, (__attribute__((address_space(3))) void*)(vt + n * 1024), 16, voff, 0, 0, 0);
+    }
+  }
+};
+
+__device__ __forceinline__ void wait_vm() {
+  // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 s_waitcnt encoding).
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+}
 
 // One 64-key tile of the forward for one wave (32 query rows): S^T = K·Q^T, masks, online
 // softmax (lazy rescale), O^T += V^T·P^T.  Shared by the single-block and pair kernels.
@@ -240,18 +289,33 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_fast_kernel(FwdParams p) {
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
 
   if (kbeg < kend) {
-    st.load(kbeg);
-    st.template store<E>(kb0, vb0, kzp, vzp);
+    if constexpr (KVSRC == SRC_SAME) {
+      st.issue(kbeg, kb0, vb0);
+      wait_vm();
+    } else {
+      st.load(kbeg);
+      st.template store<E>(kb0, vb0, kzp, vzp);
+    }
   }
   __syncthreads();
 
   int cur = 0;
   for (int t = kbeg; t < kend; t += BK) {
     const bool has_next = t + BK < kend;
-    if (has_next) st.load(t + BK);
+    if constexpr (KVSRC == SRC_SAME) {
+      // The other buffer was last read in the previous iteration (barrier since).
+      if (has_next) st.issue(t + BK, kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB);
+    } else {
+      if (has_next) st.load(t + BK);
+    }
     fwd_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, qf, o, m, lh, t, q0, qi, p, c,
                         wsz, lane);
-    if (has_next) st.template store<E>(kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB, kzp, vzp);
+    if constexpr (KVSRC == SRC_SAME) {
+      wait_vm();
+    } else {
+      if (has_next)
+        st.template store<E>(kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB, kzp, vzp);
+    }
     __syncthreads();
     cur ^= 1;
   }
@@ -356,8 +420,13 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
     float m = -kFltMax, lh = 0.f;
 
     if (t0 < t1) {
-      st.load(t0);
-      st.template store<E>(kb0, vb0, kzp, vzp);
+      if constexpr (KVSRC == SRC_SAME) {
+        st.issue(t0, kb0, vb0);
+        wait_vm();
+      } else {
+        st.load(t0);
+        st.template store<E>(kb0, vb0, kzp, vzp);
+      }
     }
     __syncthreads();
     int cur = 0;
@@ -365,11 +434,19 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd_pair_kernel(FwdParams p) {
       const int t = t0 + step * BK;
       if (t < t1) {
         const bool has_next = t + BK < t1;
-        if (has_next) st.load(t + BK);
+        if constexpr (KVSRC == SRC_SAME) {
+          if (has_next) st.issue(t + BK, kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB);
+        } else {
+          if (has_next) st.load(t + BK);
+        }
         fwd_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, qf, o, m, lh, t, q0, qi, p,
                             c, wsz, lane);
-        if (has_next)
-          st.template store<E>(kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB, kzp, vzp);
+        if constexpr (KVSRC == SRC_SAME) {
+          wait_vm();
+        } else {
+          if (has_next)
+            st.template store<E>(kb0 + (cur ^ 1) * TILEB, vb0 + (cur ^ 1) * TILEB, kzp, vzp);
+        }
       }
       __syncthreads();
       cur ^= 1;
