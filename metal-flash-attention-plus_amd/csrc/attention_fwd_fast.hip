@@ -163,11 +163,23 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt,
   f32x16 s[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) s[j] = zero16();
+  {
+    // K fragments are read QK_AHEAD MFMAs ahead of their use; sched_barrier(0) pins the
+    // order (left alone, hipcc issues each read right before its MFMA and waits on it).
+    constexpr int NM = A::DSTEPS * NJ;
+    constexpr int AH = 4;
+    i16x8 kf[AH];
 #pragma unroll
-  for (int ds = 0; ds < A::DSTEPS; ++ds)
+    for (int i = 0; i < AH; ++i) kf[i] = A::read_row(kt, (i % NJ) * 32 + l32, i / NJ, hh);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      s[j] = A::mma(A::read_row(kt, j * 32 + l32, ds, hh), qf[ds], s[j]);
+    for (int i = 0; i < NM; ++i) {
+      const int ds = i / NJ, j = i % NJ;
+      s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
+      if (i + AH < NM)
+        kf[i % AH] = A::read_row(kt, ((i + AH) % NJ) * 32 + l32, (i + AH) / NJ, hh);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 
   // Masks: only tiles that reach past the diagonal / edge / window.
   const bool edge = t + BK > p.C;
@@ -225,15 +237,33 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt,
   }
   lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
 
+  {
+    // V^T fragments (two tr-reads each) PV_AHEAD MFMAs ahead, order pinned as above.
+    constexpr int ND = DP / 32;
+    constexpr int NM = NJ * 2 * ND;
+    constexpr int AH = 3;
+    i16x8 pb[NJ * 2];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const i16x8 pb = A::pack(s[j], ks);
+      for (int ks = 0; ks < 2; ++ks) pb[j * 2 + ks] = A::pack(s[j], ks);
+    i16x8 vf[AH];
 #pragma unroll
-      for (int dt = 0; dt < DP / 32; ++dt)
-        o[dt] = A::mma(A::read_tr(vt, j * 32, ks, dt * 32, lane), pb, o[dt]);
+    for (int i = 0; i < AH; ++i) {
+      const int jk = i / ND, dt = i % ND;
+      vf[i] = A::read_tr(vt, (jk >> 1) * 32, jk & 1, dt * 32, lane);
     }
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const int jk = i / ND, dt = i % ND;
+      o[dt] = A::mma(vf[i % AH], pb[jk], o[dt]);
+      if (i + AH < NM) {
+        const int jn = (i + AH) / ND, dn = (i + AH) % ND;
+        vf[i % AH] = A::read_tr(vt, (jn >> 1) * 32, jn & 1, dn * 32, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 }
 
 template <class E, int DP, int BK, int KVSRC>
