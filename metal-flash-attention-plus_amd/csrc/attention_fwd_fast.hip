@@ -89,65 +89,21 @@ struct KVStage {
   }
 };
 
-// 16-bit K/V: LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave-instruction) straight
-// into the XOR-swizzled tile, no staging registers and no ds_write.  A piece covers RP rows;
-// lane l lands at byte 16*l of it (row n*RP + l/CPR, physical chunk l%CPR) and so fetches
-// the logical chunk (l%CPR) ^ swz(row).  Wave w of the NW staging waves issues pieces
-// n = w + NW*i, and swz depends only on row & 15, so each wave needs one lane offset per
-// tensor.  Rows past the end and chunks past D read as zeros (range-checked descriptor built
-// per piece from wave-uniform values).
+// 16-bit K/V: LDS-DMA straight into the swizzled tile (mfa_stage.h TileDMA).
 template <int DP, int BK, int NT>
 struct KVStage<DP, BK, NT, SRC_SAME> {
-  using T = Tile16<DP>;
-  static constexpr int NW = NT / 64;
-  static constexpr int CPR = DP / 8;
-  static constexpr int RP = 1024 / T::ROWB;           // rows per piece
-  static constexpr int NPIECE = BK / RP;              // pieces per tile
-  static constexpr int PPW = NPIECE / NW;             // pieces per wave
-  static_assert(NPIECE % NW == 0 && (16 % RP == 0 || RP % 16 == 0), "DMA geometry");
-  static_assert((NW * RP) % 16 == 0, "one swizzle phase per wave");
-  const char* kg;
-  const char* vg;
-  int kstep, vstep, kbytes, vbytes;
-  int koff, voff, w;
-
+  TileDMA<DP * 2, BK, NT> kd, vd;
   __device__ __forceinline__ void init(const FwdParams& p, int b, int kvh, int gt) {
-    kg = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
-    vg = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
-    kstep = (int)p.k.ss * 2;
-    vstep = (int)p.v.ss * 2;
-    kbytes = (int)(((int64_t)(p.C - 1) * p.k.ss + p.D) * 2);
-    vbytes = (int)(((int64_t)(p.C - 1) * p.v.ss + p.D) * 2);
-    w = __builtin_amdgcn_readfirstlane(gt >> 6);
-    const int l = gt & 63;
-    const int rl = l / CPR, pc = l % CPR;
-    const int row = w * RP + rl;                       // row of this wave's first piece
-    const int ch = pc ^ T::swz(row);
-    const bool in = ch * 8 < p.D;
-    koff = in ? rl * kstep + ch * 16 : 0x40000000;
-    voff = in ? rl * vstep + ch * 16 : 0x40000000;
+    kd.init((const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2,
+            (int)p.k.ss * 2, p.C, p.D * 2, gt);
+    vd.init((const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2,
+            (int)p.v.ss * 2, p.C, p.D * 2, gt);
   }
   __device__ __forceinline__ void issue(int t, char* kt, char* vt) const {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int n = w + NW * i;
-      const int kb = (t + n * RP) * kstep, vb = (t + n * RP) * vstep;
-      const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(kg + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
-      const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(vg + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          krs, (__attribute__((address_space(3))) void*)(kt + n * 1024), 16, koff, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          vrs, (__attribute__((address_space(3))) void*)(vt + n * 1024), 16, voff, 0, 0, 0);
-    }
+    kd.issue(t, kt);
+    vd.issue(t, vt);
   }
 };
-
-__device__ __forceinline__ void wait_vm() {
-  // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 s_waitcnt encoding).
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-}
 
 // One 64-key tile of the forward for one wave (32 query rows): S^T = K·Q^T, masks, online
 // softmax (lazy rescale), O^T += V^T·P^T.  Shared by the single-block and pair kernels.

@@ -43,7 +43,7 @@ constexpr int WLDS = 2 * WGROUP_LDS;     // 128 KiB
 // the piece, i.e. row 4n + (l>>4), physical chunk l&15, so it fetches logical chunk
 // (l&15) ^ swz(row) — the Tile16<128> swizzle, which depends on row&3 = (l>>4)&3 and
 // (row>>2)&3 = n&3 only.
-struct TileDMA {
+struct WideDMA {
   const char* base;  // head base (bytes)
   int step;          // bytes per key row
   int bytes;         // bytes in the head (range limit)
@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_wide_kernel(FwdParams p) {
   const float c = p.c_log2;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
 
-  TileDMA kd, vd;
+  WideDMA kd, vd;
   kd.init((const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2,
           (int)p.k.ss, p.C, p.D, wq, lane);
   vd.init((const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2,

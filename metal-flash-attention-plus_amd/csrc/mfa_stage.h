@@ -312,4 +312,54 @@ __device__ __forceinline__ void load_row_frags(typename A::frag (&f)[A::DSTEPS],
   }
 }
 
+
+// LDS-DMA of one [BK rows][ROWB bytes] tile (buffer_load ... lds, one 1-KiB piece per
+// wave-instruction) straight into the Tile16 XOR-swizzled layout: no staging registers, no
+// ds_write.  A piece covers RP = 1024/ROWB rows; lane l lands at byte 16*l of it (row
+// n*RP + l/CPR, physical chunk l%CPR) and so fetches the logical chunk (l%CPR) ^ swz(row).
+// Wave w of the NT/64 staging waves issues pieces n = w + NW*i; the swizzle depends only on
+// row & 15, so each wave needs a single lane offset.  Rows past the end and chunks past the
+// row's valid bytes read as zeros: the range-checked descriptor is rebuilt per piece from
+// wave-uniform values (base at the piece's first row, num_records = bytes left).
+template <int ROWB, int BK, int NT>
+struct TileDMA {
+  using T = Tile16<ROWB / 2>;
+  static constexpr int NW = NT / 64;
+  static constexpr int CPR = ROWB / 16;
+  static constexpr int RP = 1024 / ROWB;
+  static constexpr int NPIECE = BK * ROWB / 1024;
+  static constexpr int PPW = NPIECE / NW;
+  static_assert(NPIECE % NW == 0 && (NW * RP) % 16 == 0, "DMA geometry");
+  const char* base;
+  int step, bytes, off, w;
+
+  // head: first byte of the (batch, head) slice; step: bytes per row; rowbytes: valid bytes
+  // per row (D * element size); gt: thread index within the staging waves.
+  __device__ __forceinline__ void init(const char* head, int step_, int C, int rowbytes, int gt) {
+    base = head;
+    step = step_;
+    bytes = (int)((int64_t)(C - 1) * step_ + rowbytes);
+    w = __builtin_amdgcn_readfirstlane(gt >> 6);
+    const int l = gt & 63;
+    const int rl = l / CPR, pc = l % CPR;
+    const int ch = pc ^ T::swz(w * RP + rl);
+    off = ch * 16 < rowbytes ? rl * step + ch * 16 : 0x40000000;
+  }
+  __device__ __forceinline__ void issue(int t, char* dst) const {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int n = w + NW * i;
+      const int rb = (t + n * RP) * step;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(base + rb), (short)0, max(bytes - rb, 0), 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(dst + n * 1024), 16, off, 0, 0, 0);
+    }
+  }
+};
+
+// Wait for this wave's outstanding vector-memory operations (LDS-DMA included): vmcnt(0),
+// expcnt / lgkmcnt untouched (gfx9 s_waitcnt encoding).
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 }  // namespace mfa
