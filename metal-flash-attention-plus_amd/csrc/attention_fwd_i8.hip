@@ -38,8 +38,8 @@ __device__ __forceinline__ float xh_sum(float x) {
 
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
-template <class E, int DP, int BK>
-__global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
+template <class E, int DP, int BK, int OCC>
+__global__ void __launch_bounds__(256, OCC) mfa_fwd_i8_kernel(FwdParams p) {
   static_assert(DP == 128 && BK == 64, "int8 kernel is specialised for D<=128, 64-key tiles");
   using TK = Tile16<DP / 2>;            // [BK][DP bytes] = 16-byte chunks, DP/16 per row
   constexpr int NT = 256, BQ = 128;
@@ -121,40 +121,12 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   const int8_t* kg = (const int8_t*)p.k.ptr + (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
   const int8_t* vg = (const int8_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
   constexpr int KCPR = DP / 16;  // 8 chunks per K row
-  // K/V arrive through buffer loads whose range check returns 0 past the head's last byte: the
-  // descriptor is rebuilt per tile from wave-uniform values (base at the tile's rows,
-  // num_records = bytes left), so the tail tile needs no per-lane branches or clamps.  Columns
-  // past D in a row read the next row's bytes: Q is zero there and O columns >= D are not
-  // stored.
-  const int kbytes = (int)((int64_t)(p.C - 1) * p.k.ss + p.D);
-  const int vbytes = (int)((int64_t)(p.C - 1) * p.v.ss + p.D);
-  const int kss = (int)p.k.ss, vss = (int)p.v.ss;
-  constexpr int RPI = NT / KCPR;  // rows between a thread's two chunks
-  const int koff = (tid / KCPR) * kss + (tid % KCPR) * 16;
-  const int voff = (tid / KCPR) * vss + (tid % KCPR) * 16;
-  const int lds_off = TK::off(tid / KCPR, tid % KCPR);  // chunk 1: +RPI rows, same swizzle
-  uint4 rk[2], rv[2];
-  auto load = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kb = (t + i * RPI) * kss, vb = (t + i * RPI) * vss;
-      const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(kg + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
-      const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(vg + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
-      const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, koff, 0, 0);
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0);
-      rk[i] = make_uint4(a[0], a[1], a[2], a[3]);
-      rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(kb0 + buf * KTILE + lds_off + i * RPI * TK::ROWB) = rk[i];
-      *reinterpret_cast<uint4*>(vb0 + buf * VTILE + lds_off + i * RPI * TK::ROWB) = rv[i];
-    }
-  };
+  // K/V tiles arrive by LDS-DMA straight into the swizzled layout (mfa_stage.h TileDMA);
+  // rows past the end and columns past D read as zeros (the host requires D % 16 == 0).
+  TileDMA<DP, BK, NT> kd, vd;
+  kd.init((const char*)kg, (int)p.k.ss, p.C, p.D, tid);
+  vd.init((const char*)vg, (int)p.v.ss, p.C, p.D, tid);
+
   // V^T operand via ds_read_b64_tr_b8: in each 16-lane group, lane 2j supplies the row of key
   // acc_row(j + 8r, h) at column d0, lane 2j+1 the same row at d0 + 8; lane i < 8 receives
   // column d0 + i of those 8 rows, lane 8 + i column d0 + 8 + i.
@@ -182,15 +154,19 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   float m = -kFltMax, lh = 0.f;
 
   if (kbeg < kend) {
-    load(kbeg);
-    store(0);
+    kd.issue(kbeg, kb0);
+    vd.issue(kbeg, vb0);
+    wait_vm();
   }
   __syncthreads();
 
   int cur = 0;
   for (int t = kbeg; t < kend; t += BK) {
     const bool has_next = t + BK < kend;
-    if (has_next) load(t + BK);
+    if (has_next) {  // the other buffer was last read before the previous barrier
+      kd.issue(t + BK, kb0 + (cur ^ 1) * KTILE);
+      vd.issue(t + BK, vb0 + (cur ^ 1) * VTILE);
+    }
     const char* kt = kb0 + cur * KTILE;
     const char* vt = vb0 + cur * VTILE;
 
@@ -199,13 +175,24 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) si[j][i] = 0;
+    {
+      // K fragments read AH MFMAs ahead; sched_barrier(0) pins the order.
+      constexpr int NM = KSTEPS * NJ, AH = 4;
+      i32x4 kf[AH];
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s)
+      for (int i = 0; i < AH; ++i)
+        kf[i] = *reinterpret_cast<const i32x4*>(kt + TK::off((i % NJ) * 32 + l32, 2 * (i / NJ) + hh));
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const i32x4 a = *reinterpret_cast<const i32x4*>(kt + TK::off(j * 32 + l32, 2 * s + hh));
-        si[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], si[j], 0, 0, 0);
+      for (int i = 0; i < NM; ++i) {
+        const int j = i % NJ;
+        si[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(kf[i % AH], qf[i / NJ], si[j], 0, 0, 0);
+        if (i + AH < NM) {
+          const int n = i + AH;
+          kf[i % AH] = *reinterpret_cast<const i32x4*>(kt + TK::off((n % NJ) * 32 + l32, 2 * (n / NJ) + hh));
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
+    }
 
     float sf[NJ][16];
 #pragma unroll
@@ -262,29 +249,36 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ps[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sf[j][i], cq, -mq));
     }
-    float rs = 0.f;
+    float rs[4] = {0.f, 0.f, 0.f, 0.f};
+    i32x4 pb[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      i32x4 pb;
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         uint32_t word = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          rs += ps[j][4 * k + e];
+          rs[e] += ps[j][4 * k + e];
           word = __builtin_amdgcn_cvt_pk_u8_f32(ps[j][4 * k + e], e, word);
         }
-        pb[k] = (int)word;
+        pb[j][k] = (int)word;
       }
-      // O^T += V^T · P'^T over this 32-key sub-tile (k order = accumulator registers).
+    lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
+    {
+      // O^T += V^T · P'^T (k order = accumulator registers); V^T fragments AH MFMAs ahead.
+      constexpr int ND = DP / 32, NM = NJ * ND, AH = 3;
+      i32x4 vf[AH];
 #pragma unroll
-      for (int dt = 0; dt < DP / 32; ++dt) {
-        oi[dt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(read_vt(vt, j, dt), pb, oi[dt], 0, 0, 0);
+      for (int i = 0; i < AH; ++i) vf[i] = read_vt(vt, i / ND, i % ND);
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        oi[i % ND] = __builtin_amdgcn_mfma_i32_32x32x32_i8(vf[i % AH], pb[i / ND], oi[i % ND], 0, 0, 0);
+        if (i + AH < NM) vf[i % AH] = read_vt(vt, (i + AH) / ND, (i + AH) % ND);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    lh += rs;
 
-    if (has_next) store(cur ^ 1);
+    wait_vm();
     __syncthreads();
     cur ^= 1;
   }
@@ -315,10 +309,10 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_i8_kernel(FwdParams p) {
   }
 }
 
-template <class E>
+template <class E, int OCC>
 static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 2 * (64 * 128) + 2 * (128 * 64);
-  auto kern = mfa_fwd_i8_kernel<E, 128, 64>;
+  auto kern = mfa_fwd_i8_kernel<E, 128, 64, OCC>;
   hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
   return hipGetLastError();
 }
@@ -326,8 +320,9 @@ static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
 // INT8-MFMA forward: Q fp16/bf16 (quantised per row in-kernel), K/V INT8 per-tensor with zero
 // point 0, D <= 128, D % 16 == 0.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) {
-  if (elem == P_FP16) return launch_i8<F16>(p, stream);
-  if (elem == P_BF16) return launch_i8<BF16>(p, stream);
+  // 3 waves per SIMD: the kernel fits in 168 VGPRs and 3 x 32 KiB of LDS per CU.
+  if (elem == P_FP16) return launch_i8<F16, 3>(p, stream);
+  if (elem == P_BF16) return launch_i8<BF16, 3>(p, stream);
   return hipErrorNotSupported;
 }
 
