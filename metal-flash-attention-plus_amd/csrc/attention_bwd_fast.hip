@@ -1,0 +1,565 @@
+// attention_bwd_fast.hip — the two phases of the reference's 7-GEMM backward, tuned for the
+// common case on gfx950: fp16/bf16 Q/K/V/dO with 16-byte aligned contiguous rows, D % 8 == 0,
+// D <= DP ∈ {64, 128, 256}, no mask or causal / sliding-window masks whose fully masked tiles
+// may be skipped (no additive mask, no sparse ranges).  Same algorithm and numerics contract as
+// attention_bwd.h (AttentionKernel+Source.swift:418-511, Softmax.swift:31-236 / :795-804);
+// everything else goes to that generic kernel.
+//
+// Structure (both phases): 4 waves, one per SIMD (up to 512 registers per lane), 32 rows per
+// wave held in registers for the whole kernel; the traversed operand pair streams through a
+// double-buffered LDS ring filled by LDS-DMA (buffer_load ... lds, no staging registers), one
+// barrier per tile.  Fragment reads are issued a few MFMAs ahead of their use and the order is
+// pinned with sched_barrier (left alone, hipcc issues each read right before its MFMA).
+//
+//   bwd_q  (3 GEMMs): S^T = K·Q^T, dP^T = V·dO^T (query on the lane), P^T = exp2(S^T·c − L),
+//                     dS^T = P^T∘(dP^T·scale − D), dQ^T += K^T·dS^T.  Writes D.
+//   bwd_kv (4 GEMMs): S = Q·K^T, dP = dO·V^T (key on the lane), dV^T += dO^T·P,
+//                     dK^T += Q^T·dS; sums over every query head of the kv group (GQA).
+//
+// Rows past the end need no masks: the DMA zero-fills K/V/Q/dO rows past C or R, so their
+// products vanish (bwd_q: K^T·dS^T with zero K rows; bwd_kv: L = +inf gives P = dS = 0 for
+// query rows past R, and key lanes past C are never stored).  Only the causal / window
+// diagonal tiles run the mask code; with skip_ok no row is masked everywhere, so
+// exp2(S·c − L) needs no mask-level special case.
+#include "mfa_stage.h"
+#include "mfa_dispatch.h"
+
+namespace mfa {
+
+// LDS-DMA of one [ROWS][DP] 16-bit tile into the TileA image (buffer_load ... lds, one 1-KiB
+// piece per wave-instruction, lane l landing at byte 16*l of its piece), for a base pointer
+// that may change from tile to tile (the kv group's query heads).  Piece n is half of 8-row
+// block n / (DP/64): its two 512-B sub-tiles (column blocks 2*(n % (DP/64)) and +1), so lane
+// l fetches row 8*(n / (DP/64)) + (l & 31)/4, logical chunk 4*sub + ((l & 3) ^ ((row>>2)&3)).
+// Rows past nrows and chunks past rowbytes read as zeros (range-checked descriptor rebuilt
+// per piece from wave-uniform values; out-of-row chunks get an out-of-range offset).
+template <int DP, int ROWS, int NT>
+struct DmaA {
+  static constexpr int NW = NT / 64;
+  static constexpr int PPRB = DP / 64;                 // pieces per 8-row block
+  static constexpr int NPIECE = ROWS * DP * 2 / 1024;
+  static constexpr int PPW = NPIECE / NW;
+  static_assert(DP % 64 == 0 && NPIECE % NW == 0 && PPW >= 1, "DMA geometry");
+  int step, bytes, w;
+  int off[PPW];
+
+  __device__ __forceinline__ void init(int step_, int nrows, int rowbytes, int gt) {
+    step = step_;
+    bytes = (int)((int64_t)(nrows - 1) * step_ + rowbytes);
+    w = __builtin_amdgcn_readfirstlane(gt >> 6);
+    const int l = gt & 63;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int n = w + NW * i;
+      const int rblk = n / PPRB, sub = 2 * (n % PPRB) + (l >> 5);
+      const int r7 = (l & 31) >> 2;
+      const int ch = 4 * sub + ((l & 3) ^ ((2 * rblk + (r7 >> 2)) & 3));
+      off[i] = ch * 16 < rowbytes ? (rblk * 8 + r7) * step + ch * 16 : 0x40000000;
+    }
+  }
+  __device__ __forceinline__ void issue(const char* head, int t, char* dst) const {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int n = w + NW * i;
+      const int rb = t * step;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(head + rb), (short)0, max(bytes - rb, 0), 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(dst + n * 1024), 16, off[i], 0, 0, 0);
+    }
+  }
+};
+
+// Row fragments of one row (16-bit, contiguous): elements d = 16*s + 8*hh + j.
+template <int DP>
+__device__ __forceinline__ void load_frags16(i16x8 (&f)[DP / 16], const uint16_t* row, bool valid,
+                                             int D, int hh) {
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    f[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (valid && d0 < D) f[s] = *reinterpret_cast<const i16x8*>(row + d0);
+  }
+}
+
+// Two MFMA chains over the head dimension sharing the register operand index:
+//   acc1[j] += A1(rows j*32..) · b1[ds],  acc2[j] += A2(rows j*32..) · b2[ds]
+// with A fragments read from LDS row tiles AH instructions ahead of their MFMA.
+template <class A, int NJ>
+__device__ __forceinline__ void dual_rows_chain(const char* t1, const char* t2,
+                                                const i16x8* b1, const i16x8* b2,
+                                                f32x16 (&acc1)[NJ], f32x16 (&acc2)[NJ],
+                                                const int (&rbase)[2]) {
+  constexpr int NM = A::DSTEPS * NJ * 2;
+  constexpr int AH = 4;
+  i16x8 fr[AH];
+  auto rd = [&](int i) {
+    const int pair = i >> 1, which = i & 1;
+    const int ds = pair / NJ, j = pair % NJ;
+    return A::read_row_a(which ? t2 : t1, rbase, j, ds);
+  };
+#pragma unroll
+  for (int i = 0; i < AH; ++i) fr[i] = rd(i);
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const int pair = i >> 1, which = i & 1;
+    const int ds = pair / NJ, j = pair % NJ;
+    if (which)
+      acc2[j] = A::mma(fr[i % AH], b2[ds], acc2[j]);
+    else
+      acc1[j] = A::mma(fr[i % AH], b1[ds], acc1[j]);
+    if (i + AH < NM) fr[i % AH] = rd(i + AH);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backwardQuery.  Grid: nblk x B x H, heaviest causal blocks first.  BT keys per tile.
+template <class E, int DP, int BT>
+__global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
+  using A = Arith16<E, DP>;
+  constexpr int NT = 256, BQ = 128, NJ = BT / 32, DS = DP / 16, ND = DP / 32;
+  constexpr int TILEB = BT * DP * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const kb0 = smem;
+  char* const vb0 = smem + 2 * TILEB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
+  const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
+  const int BH = p.B * p.H;
+  const int bid = blockIdx.x;
+  const int rb = p.nblk - 1 - bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
+  const int q0 = rb * BQ;
+  const int qi = q0 + wave * 32 + l32;
+  const bool qvalid = qi < p.R;
+  const int64_t row = (int64_t)(b * p.H + h) * p.R + qi;
+
+  i16x8 qf[DS], dof[DS];
+  {
+    const int qq = qvalid ? qi : 0;
+    load_frags16<DP>(qf, (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh +
+                             (int64_t)qq * p.q.ss, qvalid, p.D, hh);
+    load_frags16<DP>(dof, (const uint16_t*)p.dO_op.ptr + (int64_t)b * p.dO_op.sb +
+                              (int64_t)h * p.dO_op.sh + (int64_t)qq * p.dO_op.ss,
+                     qvalid, p.D, hh);
+  }
+
+  // K/V ring: issue the first tile before the D prologue so its latency hides behind it.
+  int kend = p.C;
+  if (p.mask.causal && p.mask.skip_ok) kend = min(kend, q0 + BQ);
+  int kbeg = 0;
+  if (p.mask.window && p.mask.skip_ok) {
+    const int64_t lo = (int64_t)q0 - (int64_t)p.mask.window_size;
+    kbeg = lo > 0 ? (int)(lo / BT) * BT : 0;
+  }
+  DmaA<DP, BT, NT> kd, vd;
+  kd.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
+  vd.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
+  const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
+  const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
+  if (kbeg < kend) {
+    kd.issue(khead, kbeg, kb0);
+    vd.issue(vhead, kbeg, vb0);
+  }
+
+  // D = scale · Σ_d dO∘O (computeD, Softmax.swift:31-236): dO as stored (16-bit), O fp32.
+  float dsum = 0.f;
+  if (qvalid) {
+    const float* orow = p.o + row * p.D;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      const int d0 = 16 * s + 8 * hh;
+      if (d0 < p.D) {
+        const float4 oa = *reinterpret_cast<const float4*>(orow + d0);
+        const float4 ob = *reinterpret_cast<const float4*>(orow + d0 + 4);
+        const float ov[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += E::to_f32((uint16_t)dof[s][j]) * ov[j];
+      }
+    }
+  }
+  dsum = cross_half_sum(dsum);
+  const float Drow = p.dscale * dsum;
+  float Lrow = __builtin_inff();
+  if (qvalid) {
+    Lrow = p.l_f16 ? f16_to_f32(reinterpret_cast<const uint16_t*>(p.l)[row])
+                   : reinterpret_cast<const float*>(p.l)[row];
+    if (hh == 0) {
+      if (p.d_bf16)  // BF16 memory form = upper half of the FP32 bits (Caching.swift:413-421)
+        reinterpret_cast<uint16_t*>(p.dD)[row] = (uint16_t)(__builtin_bit_cast(uint32_t, Drow) >> 16);
+      else
+        reinterpret_cast<float*>(p.dD)[row] = Drow;
+    }
+  }
+  const float c = p.c_log2, sc = p.scale;
+  const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+
+  f32x16 dq[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) dq[dt] = zero16();
+
+  wait_vm();
+  __syncthreads();
+  int cur = 0;
+  for (int t = kbeg; t < kend; t += BT) {
+    if (t + BT < kend) {
+      kd.issue(khead, t + BT, kb0 + (cur ^ 1) * TILEB);
+      vd.issue(vhead, t + BT, vb0 + (cur ^ 1) * TILEB);
+    }
+    const char* kt = kb0 + cur * TILEB;
+    const char* vt = vb0 + cur * TILEB;
+    f32x16 s[NJ], dp[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { s[j] = zero16(); dp[j] = zero16(); }
+    dual_rows_chain<A, NJ>(kt, vt, qf, dof, s, dp, rbase);
+
+    const bool diag = (p.mask.causal && t + BT - 1 > q0) || p.mask.window;
+    if (diag) {
+      MFA_KEEP_BRANCH();
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = t + j * 32 + acc_row(i, hh);
+          if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) s[j][i] = kMaskValue;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -Lrow));
+        dp[j][i] = pv * __builtin_fmaf(dp[j][i], sc, -Drow);
+      }
+
+    // dQ^T += K^T · dS^T (K^T by transposed reads), reads AH MFMAs ahead.
+    {
+      constexpr int NM = NJ * 2 * ND;
+      constexpr int AH = 3;
+      i16x8 sb[NJ * 2];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) sb[j * 2 + ks] = A::pack(dp[j], ks);
+      i16x8 kf[AH];
+#pragma unroll
+      for (int i = 0; i < AH; ++i) {
+        const int jk = i / ND, dt = i % ND;
+        kf[i] = A::read_tr_a(kt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
+      }
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        const int jk = i / ND, dt = i % ND;
+        dq[dt] = A::mma(kf[i % AH], sb[jk], dq[dt]);
+        if (i + AH < NM) {
+          const int jn = (i + AH) / ND, dn = (i + AH) % ND;
+          kf[i % AH] = A::read_tr_a(kt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    wait_vm();
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  if (qvalid) {
+    float* out = p.dq + row * p.D;
+    const float mul = p.dq_mul;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        if (d < p.D)
+          *reinterpret_cast<float4*>(out + d) =
+              make_float4(dq[dt][4 * g] * mul, dq[dt][4 * g + 1] * mul, dq[dt][4 * g + 2] * mul,
+                          dq[dt][4 * g + 3] * mul);
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backwardKeyValue.  Grid: nblk x B x H_kv (first key blocks carry the most causal query
+// tiles).  128 keys per workgroup; BQ query rows per step.
+template <class E, int DP, int BQ>
+__global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
+  using A = Arith16<E, DP>;
+  constexpr int NT = 256, BK = 128, NJ = BQ / 32, DS = DP / 16, ND = DP / 32;
+  constexpr int TILEB = BQ * DP * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const qb0 = smem;
+  char* const ob0 = smem + 2 * TILEB;
+  float* const lb0 = reinterpret_cast<float*>(smem + 4 * TILEB);  // [2][BQ] L, then [2][BQ] D
+  float* const db0 = lb0 + 2 * BQ;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
+  const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
+  const int BH = p.B * p.Hkv;
+  const int bid = blockIdx.x;
+  const int kb = bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / p.Hkv, kvh = bh % p.Hkv;
+  const int k0 = kb * BK;
+  const int ki = k0 + wave * 32 + l32;
+  const bool kvalid = ki < p.C;
+
+  i16x8 kf[DS], vf[DS];
+  {
+    const int kk = kvalid ? ki : 0;
+    load_frags16<DP>(kf, (const uint16_t*)p.k.ptr + (int64_t)b * p.k.sb +
+                             (int64_t)kvh * p.k.sh + (int64_t)kk * p.k.ss, kvalid, p.D, hh);
+    load_frags16<DP>(vf, (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb +
+                             (int64_t)kvh * p.v.sh + (int64_t)kk * p.v.ss, kvalid, p.D, hh);
+  }
+
+  int qbeg = 0, qend = p.R;
+  if (p.mask.causal && p.mask.skip_ok) qbeg = (k0 / BQ) * BQ;
+  if (p.mask.window && p.mask.skip_ok) {
+    const int64_t hi = (int64_t)k0 + BK + (int64_t)p.mask.window_size;
+    if (hi < qend) qend = (int)hi;
+  }
+  const int ntile = qbeg < qend ? (qend - qbeg + BQ - 1) / BQ : 0;
+  const int ngroup = (p.H - kvh + p.Hkv - 1) / p.Hkv;  // query heads h = kvh + g*Hkv
+  const int nsteps = ntile * ngroup;
+
+  DmaA<DP, BQ, NT> qd, od;
+  qd.init((int)p.q.ss * 2, p.R, p.D * 2, tid);
+  od.init((int)p.dO_op.ss * 2, p.R, p.D * 2, tid);
+  auto qhead = [&](int h) {
+    return (const char*)p.q.ptr + ((int64_t)b * p.q.sb + (int64_t)h * p.q.sh) * 2;
+  };
+  auto ohead = [&](int h) {
+    return (const char*)p.dO_op.ptr + ((int64_t)b * p.dO_op.sb + (int64_t)h * p.dO_op.sh) * 2;
+  };
+  // L and D of the step's BQ query rows: one value per thread of the first BQ threads, staged
+  // through registers into LDS (converted to fp32); L = +inf past R makes P = dS = 0 there.
+  float lreg = 0.f, dreg = 0.f;
+  auto ld_load = [&](int h, int t) {
+    if (tid < BQ) {
+      const int q = t + tid;
+      const int64_t r = (int64_t)(b * p.H + h) * p.R + q;
+      lreg = __builtin_inff();
+      dreg = 0.f;
+      if (q < p.R) {
+        lreg = p.l_f16 ? f16_to_f32(reinterpret_cast<const uint16_t*>(p.l)[r])
+                       : reinterpret_cast<const float*>(p.l)[r];
+        dreg = p.d_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p.dD)[r])
+                        : reinterpret_cast<const float*>(p.dD)[r];
+      }
+    }
+  };
+  auto ld_store = [&](int buf) {
+    if (tid < BQ) {
+      lb0[buf * BQ + tid] = lreg;
+      db0[buf * BQ + tid] = dreg;
+    }
+  };
+
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+  const float c = p.c_log2, sc = p.scale;
+  const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+
+  if (nsteps > 0) {
+    qd.issue(qhead(kvh), qbeg, qb0);
+    od.issue(ohead(kvh), qbeg, ob0);
+    ld_load(kvh, qbeg);
+    wait_vm();
+    ld_store(0);
+  }
+  __syncthreads();
+
+  int cur = 0;
+  for (int step = 0; step < nsteps; ++step) {
+    const int g = step / ntile;
+    const int t = qbeg + (step - g * ntile) * BQ;
+    const bool has_next = step + 1 < nsteps;
+    if (has_next) {
+      const int gn = (step + 1) / ntile;
+      const int tn = qbeg + (step + 1 - gn * ntile) * BQ;
+      const int hn = kvh + gn * p.Hkv;
+      qd.issue(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB);
+      od.issue(ohead(hn), tn, ob0 + (cur ^ 1) * TILEB);
+      ld_load(hn, tn);
+    }
+    const char* qt = qb0 + cur * TILEB;
+    const char* ot = ob0 + cur * TILEB;
+    const float* lt = lb0 + cur * BQ;
+    const float* dtl = db0 + cur * BQ;
+
+    f32x16 s[NJ], dp[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { s[j] = zero16(); dp[j] = zero16(); }
+    dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase);
+
+    const bool diag = (p.mask.causal && k0 + BK - 1 > t) || p.mask.window;
+    if (diag) {
+      MFA_KEEP_BRANCH();
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = t + j * 32 + acc_row(i, hh);
+          if ((p.mask.causal && ki > q) || (p.mask.window && q - ki > wsz)) s[j][i] = kMaskValue;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int r0 = j * 32 + 8 * g4 + 4 * hh;
+        const float4 l4 = *reinterpret_cast<const float4*>(lt + r0);
+        const float4 d4 = *reinterpret_cast<const float4*>(dtl + r0);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -lv[e]));
+          s[j][i] = pv;
+          dp[j][i] = pv * __builtin_fmaf(dp[j][i], sc, -dv4[e]);
+        }
+      }
+
+    // dV^T += dO^T · P and dK^T += Q^T · dS (transposed reads of the row tiles).
+    {
+      constexpr int NM = NJ * 2 * ND * 2;
+      constexpr int AH = 4;
+      i16x8 pb[NJ * 2], sb[NJ * 2];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          pb[j * 2 + ks] = A::pack(s[j], ks);
+          sb[j * 2 + ks] = A::pack(dp[j], ks);
+        }
+      auto rd = [&](int i) {
+        const int pair = i >> 1, which = i & 1;
+        const int jk = pair / ND, dt = pair % ND;
+        return A::read_tr_a(which ? qt : ot, trb, (jk >> 1) * 32, jk & 1, dt * 32);
+      };
+      i16x8 fr[AH];
+#pragma unroll
+      for (int i = 0; i < AH; ++i) fr[i] = rd(i);
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        const int pair = i >> 1, which = i & 1;
+        const int jk = pair / ND, dt = pair % ND;
+        if (which)
+          dk[dt] = A::mma(fr[i % AH], sb[jk], dk[dt]);
+        else
+          dv[dt] = A::mma(fr[i % AH], pb[jk], dv[dt]);
+        if (i + AH < NM) fr[i % AH] = rd(i + AH);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    wait_vm();
+    if (has_next) ld_store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  if (kvalid) {
+    const int64_t krow = (int64_t)(b * p.Hkv + kvh) * p.C + ki;
+    float* ok = p.dk + krow * p.D;
+    float* ov = p.dv + krow * p.D;
+    const float mul = p.dk_mul;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        if (d < p.D) {
+          *reinterpret_cast<float4*>(ok + d) =
+              make_float4(dk[dt][4 * g] * mul, dk[dt][4 * g + 1] * mul, dk[dt][4 * g + 2] * mul,
+                          dk[dt][4 * g + 3] * mul);
+          *reinterpret_cast<float4*>(ov + d) =
+              make_float4(dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+        }
+      }
+  }
+}
+
+template <int DP> struct BwdFastCfg {
+  static constexpr int BT = DP >= 256 ? 32 : 64;  // bwd_q key tile
+  static constexpr int BQ = DP >= 256 ? 32 : 64;  // bwd_kv query tile
+};
+
+template <class E, int DP>
+static hipError_t launch_bwd_q_fast(const BwdParams& p, hipStream_t stream) {
+  constexpr int BT = BwdFastCfg<DP>::BT;
+  constexpr int LDS = 4 * BT * DP * 2;
+  auto kern = mfa_bwd_q_fast_kernel<E, DP, BT>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  BwdParams q = p;
+  q.nblk = (p.R + 127) / 128;
+  hipLaunchKernelGGL(kern, dim3(q.nblk * p.B * p.H), dim3(256), LDS, stream, q);
+  return hipGetLastError();
+}
+
+template <class E, int DP>
+static hipError_t launch_bwd_kv_fast(const BwdParams& p, hipStream_t stream) {
+  constexpr int BQ = BwdFastCfg<DP>::BQ;
+  constexpr int LDS = 4 * BQ * DP * 2 + 4 * BQ * 4;
+  auto kern = mfa_bwd_kv_fast_kernel<E, DP, BQ>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  BwdParams q = p;
+  q.nblk = (p.C + 127) / 128;
+  hipLaunchKernelGGL(kern, dim3(q.nblk * p.B * p.Hkv), dim3(256), LDS, stream, q);
+  return hipGetLastError();
+}
+
+// kind: 0 = backwardQuery, 1 = backwardKeyValue.  hipErrorNotSupported when not covered.
+hipError_t bwd_fast_dispatch(const BwdParams& p, int kind, int elem, int DP, hipStream_t stream) {
+#define MFA_BF(ELEM, EE, DPV)                                                       \
+  if (elem == ELEM && DP == DPV)                                                    \
+    return kind == 0 ? launch_bwd_q_fast<EE, DPV>(p, stream)                        \
+                     : launch_bwd_kv_fast<EE, DPV>(p, stream);
+  MFA_BF(P_FP16, F16, 64)
+  MFA_BF(P_FP16, F16, 128)
+  MFA_BF(P_FP16, F16, 256)
+  MFA_BF(P_BF16, BF16, 64)
+  MFA_BF(P_BF16, BF16, 128)
+  MFA_BF(P_BF16, BF16, 256)
+#undef MFA_BF
+  return hipErrorNotSupported;
+}
+
+}  // namespace mfa
+
+// Explicit instantiations: hipcc does not emit every host-side kernel stub that the dispatch
+// table above references when the kernels are only named through the launch templates.
+namespace mfa {
+#define MFA_BF_INST(EE, DPV)                                                                   \
+  template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT>(BwdParams);   \
+  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ>(BwdParams);
+MFA_BF_INST(F16, 64)
+MFA_BF_INST(F16, 128)
+MFA_BF_INST(F16, 256)
+MFA_BF_INST(BF16, 64)
+MFA_BF_INST(BF16, 128)
+MFA_BF_INST(BF16, 256)
+#undef MFA_BF_INST
+}  // namespace mfa

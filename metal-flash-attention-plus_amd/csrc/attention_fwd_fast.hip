@@ -22,17 +22,6 @@
 
 namespace mfa {
 
-__device__ __forceinline__ float cross_half_max(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
-                                                  __builtin_bit_cast(unsigned, x), false, false);
-  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
-}
-__device__ __forceinline__ float cross_half_sum(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
-                                                  __builtin_bit_cast(unsigned, x), false, false);
-  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-}
-
 // K/V tile staging through range-checked buffer loads.  The descriptor is rebuilt per tile
 // from wave-uniform values (base advanced to the tile's first row, num_records = the bytes
 // left in the head), so rows past the end and chunks past D (offset forced out of range)

@@ -673,24 +673,50 @@ namespace {
 
 enum BwdPhase { PHASE_QUERY = 1, PHASE_KV = 2, PHASE_BOTH = 3 };
 
+// The tuned backward kernels (attention_bwd_fast.hip) cover 16-bit Q/K/V/dO with contiguous
+// 16-byte aligned rows, D % 8 == 0, and no mask or skippable causal / window masks.
+bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int qsrc) {
+  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+    if (e[0] == '1') return false;
+  }
+  if (elem != 1 && elem != 2) return false;
+  if (DP != 64 && DP != 128 && DP != 256) return false;
+  if (ksrc != 0 || qsrc != 0 || p.D % 8 != 0) return false;
+  const int prec = elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16;
+  for (const mfa::Operand* op : {&p.q, &p.k, &p.v, &p.dO_op}) {
+    if (op->prec != prec || !op->vec || op->sd != 1 || op->bscale) return false;
+  }
+  if (p.mask.amask || p.mask.ranges) return false;
+  if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok) return false;
+  // Tiles are addressed per head with 32-bit buffer offsets.
+  const int64_t lim = (int64_t)1 << 31;
+  if ((int64_t)p.C * p.k.ss * 2 >= lim || (int64_t)p.C * p.v.ss * 2 >= lim ||
+      (int64_t)p.R * p.q.ss * 2 >= lim || (int64_t)p.R * p.dO_op.ss * 2 >= lim)
+    return false;
+  return true;
+}
+
 mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ksrc, int qsrc,
                           int phase, hipStream_t stream) {
   mfa::BwdParams p = base_p;
   int bp, bt, nw;
   mfa::bwd_block_config(elem, DP, &bp, &bt, &nw);
+  const bool fast = bwd_fast_eligible(p, elem, DP, ksrc, qsrc);
   if (phase & PHASE_QUERY) {
     p.nblk = (p.R + bp - 1) / bp;
     if (p.R > 0) {
-      mfa_status_t st = hip_status(mfa::bwd_q_dispatch(p, elem, DP, ksrc, ksrc, stream),
-                                   "mfa_bwd_q launch");
+      hipError_t e = fast ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream) : hipErrorNotSupported;
+      if (e == hipErrorNotSupported) e = mfa::bwd_q_dispatch(p, elem, DP, ksrc, ksrc, stream);
+      mfa_status_t st = hip_status(e, "mfa_bwd_q launch");
       if (st != MFA_SUCCESS) return st;
     }
   }
   if (phase & PHASE_KV) {
     p.nblk = (p.C + bp - 1) / bp;
     if (p.C > 0) {
-      mfa_status_t st = hip_status(mfa::bwd_kv_dispatch(p, elem, DP, ksrc, qsrc, stream),
-                                   "mfa_bwd_kv launch");
+      hipError_t e = fast ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream) : hipErrorNotSupported;
+      if (e == hipErrorNotSupported) e = mfa::bwd_kv_dispatch(p, elem, DP, ksrc, qsrc, stream);
+      mfa_status_t st = hip_status(e, "mfa_bwd_kv launch");
       if (st != MFA_SUCCESS) return st;
     }
   }

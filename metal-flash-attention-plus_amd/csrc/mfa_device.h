@@ -107,6 +107,40 @@ struct Tile16 {
   static constexpr int bytes(int rows) { return rows * ROWB; }
 };
 
+// "Sub-tiled" LDS image of a [rows][DP] 16-bit tile (cdna_hip_programming.md T10, image (a)):
+// 8-row x 32-column sub-tiles of 512 B, ordered [row / 8][column / 32]; inside a sub-tile,
+// row r's four 16-byte chunks sit at 64*(r & 7) + 16*(c ^ ((r >> 2) & 3)).  Every fragment
+// read of a 32x32x16 operand, by rows (ds_read_b128) or transposed (ds_read_b64_tr_b16), is
+// then one per-lane base register plus an immediate: 2 bases cover all row reads of a
+// 32-row tile and 2 all transposed reads, where the plain swizzled rows of Tile16 need
+// a register per chunk.  Both reads are bank-conflict free.
+template <int DP>
+struct TileA {
+  static constexpr int NC = DP / 8;        // 16-byte chunks per row
+  static constexpr int RB = 16 * DP;       // bytes per 8-row block
+  static_assert(DP % 32 == 0, "TileA needs whole 32-column sub-tiles");
+  __device__ static __forceinline__ int off(int r, int ch) {
+    return RB * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+  }
+  // Row-read bases for lane (l32, hh): parity `par` of the k-step s (chunk 2s + hh).
+  __device__ static __forceinline__ int row_base(int l32, int hh, int par) {
+    return RB * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 * par + hh) ^ ((l32 >> 2) & 3));
+  }
+  // Row operand of k-step s for rows 32*j + l32: base row_base(.., s & 1).
+  __device__ static __forceinline__ const char* row_addr(const char* tile, const int (&rbase)[2],
+                                                         int j, int s) {
+    return tile + rbase[s & 1] + RB * 4 * j + 512 * (s >> 1);
+  }
+  // Transposed-read bases for lane: 16-lane group g, row q = i >> 2, columns 4*(i & 3).
+  // `half` 0 reads rows 4h + q of an 8-row block, half 1 the rows 8 further (the block after
+  // it), whose chunk swizzle differs by 2.
+  __device__ static __forceinline__ int tr_base(int lane, int half) {
+    const int h = (lane >> 5) & 1, g = (lane >> 4) & 1, i = lane & 15;
+    return 64 * (4 * h + (i >> 2)) + 16 * ((2 * g + ((i >> 1) & 1)) ^ (h ^ (2 * half))) +
+           8 * (i & 1);
+  }
+};
+
 // Arithmetic policy for 16-bit operands (f16 or bf16 MFMA, K = 16 per instruction).
 template <class E, int DP>
 struct Arith16 {
@@ -147,6 +181,25 @@ struct Arith16 {
     f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
     f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
     return f;
+  }
+  // read_tr on a TileA image: k-step s of the 32-key sub-tile at row kb, columns dcol..+31.
+  // trb = {TileA::tr_base(lane, 0), TileA::tr_base(lane, 1)}.
+  __device__ static __forceinline__ frag read_tr_a(const char* tile, const int (&trb)[2], int kb,
+                                                  int s, int dcol) {
+    constexpr int RB = TileA<DP>::RB;
+    const int o = RB * (kb / 8 + 2 * s) + 512 * (dcol / 32);
+    i16x4_tr lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) i16x4_tr*)(tile + trb[0] + o));
+    i16x4_tr hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) i16x4_tr*)(tile + trb[1] + o + RB));
+    frag f;
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+    f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+    return f;
+  }
+  __device__ static __forceinline__ frag read_row_a(const char* tile, const int (&rbase)[2],
+                                                   int j, int s) {
+    return *reinterpret_cast<const i16x8*>(TileA<DP>::row_addr(tile, rbase, j, s));
   }
   // Accumulator registers 8s..8s+7 rounded to 16-bit: the B operand of k-step s.
   __device__ static __forceinline__ frag pack(const f32x16& p, int s) {
@@ -222,5 +275,17 @@ __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >
 // Max / sum across the two 32-lane halves (lanes l and l^32 hold the same column).
 __device__ __forceinline__ float xhalf_max(float x) { return fmaxf(x, __shfl_xor(x, 32)); }
 __device__ __forceinline__ float xhalf_sum(float x) { return x + __shfl_xor(x, 32); }
+
+// The same reductions through v_permlane32_swap (no LDS round trip; lanes l and l^32 swap).
+__device__ __forceinline__ float cross_half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                                  __builtin_bit_cast(unsigned, x), false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ __forceinline__ float cross_half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                                  __builtin_bit_cast(unsigned, x), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
 
 }  // namespace mfa
