@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--no-int8", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--no-mla", action="store_true")
+    ap.add_argument("--c5-batch", type=int, default=8)
     return ap.parse_args()
 
 
@@ -112,10 +115,11 @@ def main():
     value = total_flops / elapsed / 1e12
     achieved = flops_step / (kernel_ms * 1e-3) / 1e12
 
-    # The variant the library picks for this shape (mfa_api.cpp launch_forward: causal with
-    # <= 768 row blocks runs the mirrored-pair kernel).
-    kname = ("mfa_fwd_pair_kernel<F16, 128, 64, 0>" if (S + 127) // 128 * H * B <= 768
-             else "mfa_fwd_fast_kernel<F16, 128, 64, 0>")
+    # The variant the library picks for this shape (mfa_api.cpp launch_forward ->
+    # attention_fwd_v2.hip fwd2_dispatch: causal with <= 768 row blocks runs the mirrored-pair
+    # kernel, otherwise one 128-row block per workgroup).
+    kname = ("mfa_fwd2_pair_kernel<F16, 128, 64>" if (S + 127) // 128 * H * B <= 768
+             else "mfa_fwd2_kernel<F16, 128, 64, 2>")
     result = {
         "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
         "value": round(value, 2),
@@ -197,6 +201,76 @@ def main():
             "fp16_ms": round(ms_f16, 4),
         }
         del qf, kf, vf, o3, l3, kq, vq, kh, vh
+
+    # ---------------------------------------------------------------- C5: fwd + bwd, D=256
+    if not args.no_c5:
+        B5, H5, S5, D5 = args.c5_batch, 32, 4096, 256
+        q5, k5, v5, do5 = (uniform((B5, H5, S5, D5), torch.float16) for _ in range(4))
+        o5 = torch.empty((B5, H5, S5, D5), dtype=torch.float32, device=dev)
+        l5 = torch.empty((B5, H5, S5), dtype=torch.float16, device=dev)
+        dq5, dk5, dv5 = (torch.empty_like(o5) for _ in range(3))
+        db5 = torch.empty((B5, H5, S5), dtype=torch.bfloat16, device=dev)
+        base5 = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16)
+        desc5 = mfa.MultiHeadDescriptor.make(base5, B5, H5, S5, D5)
+
+        def step5():
+            mha.forward(desc5, q5, k5, v5, o5, l5, stream=stream)
+            mha.backward(desc5, q5, k5, v5, o5, do5, l5, dq5, dk5, dv5, db5, stream=stream)
+
+        n5 = max(2, args.steps // 5)
+        step5()
+        barrier()
+        t5 = time.perf_counter()
+        for _ in range(n5):
+            step5()
+        barrier()
+        el5 = max_over_ranks(time.perf_counter() - t5)
+        f5 = (mfa.attention_flops(B5, H5, S5, S5, D5) +
+              mfa.attention_flops(B5, H5, S5, S5, D5, kind="backward"))
+        result["fwd_bwd_d256"] = {
+            "workload": f"BASELINE configs[4] shard: fp16 fwd+bwd (bwdQ then bwdKV, 7 GEMMs), "
+                        f"B={B5} per GPU (64 over 8 GPUs), H32 S4096 D256, non-causal",
+            "tflops": round(f5 * n5 * world / el5 / 1e12, 2),
+            "roofline_frac": round(f5 * n5 / el5 / 1e12 / PEAK_FP16_TFLOPS, 4),
+            "flop_convention": "4*D (fwd) + 10*D (bwd) per pair; the 7-GEMM backward executes 14*D",
+            "ms_per_step": round(el5 / n5 * 1e3, 3),
+        }
+        del q5, k5, v5, do5, o5, l5, dq5, dk5, dv5, db5
+
+    # ---------------------------------------------------------------- C4: MLA
+    if not args.no_mla:
+        B4, H4, S4, D4, LAT = 1, 16, 4096, 128, 512
+        lat = uniform((B4 * S4, LAT), torch.bfloat16)
+        wk = (uniform((LAT, H4 * D4), torch.float32) * 0.176).to(torch.bfloat16)
+        wv = (uniform((LAT, H4 * D4), torch.float32) * 0.176).to(torch.bfloat16)
+        q4 = uniform((B4, H4, S4, D4), torch.bfloat16)
+        o4 = torch.empty((B4, H4, S4, D4), dtype=torch.float32, device=dev)
+        kb4 = torch.empty((B4 * S4, H4 * D4), dtype=torch.bfloat16, device=dev)
+        vb4 = torch.empty_like(kb4)
+        base4 = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.BF16)
+
+        def step4():
+            mfa.mla_forward(base4, lat, wk, wv, q4, o4, B4, H4, S4, S4, D4, LAT,
+                            mfa.Precision.BF16, k_buf=kb4, v_buf=vb4, stream=stream)
+
+        for _ in range(2):
+            step4()
+        barrier()
+        t4 = time.perf_counter()
+        n4 = max(3, args.steps // 2)
+        for _ in range(n4):
+            step4()
+        barrier()
+        el4 = max_over_ranks(time.perf_counter() - t4)
+        f4 = 2 * (2 * B4 * S4 * LAT * H4 * D4) + mfa.attention_flops(B4, H4, S4, S4, D4)
+        result["mla"] = {
+            "workload": "BASELINE configs[3]: mlaCompressed bf16, latent 512 -> 16 heads x 128 "
+                        "(K, V decompression GEMMs + attention), S4096, non-causal",
+            "tflops": round(f4 * n4 * world / el4 / 1e12, 2),
+            "roofline_frac": round(f4 * n4 / el4 / 1e12 / PEAK_FP16_TFLOPS, 4),
+            "ms_per_step": round(el4 / n4 * 1e3, 4),
+        }
+        del lat, wk, wv, q4, o4, kb4, vb4
 
     # ---------------------------------------------------------------- CPU baseline
     if rank == 0 and not args.no_cpu:

@@ -26,50 +26,6 @@
 
 namespace mfa {
 
-// LDS-DMA of one [ROWS][DP] 16-bit tile into the TileA image (buffer_load ... lds, one 1-KiB
-// piece per wave-instruction, lane l landing at byte 16*l of its piece), for a base pointer
-// that may change from tile to tile (the kv group's query heads).  Piece n is half of 8-row
-// block n / (DP/64): its two 512-B sub-tiles (column blocks 2*(n % (DP/64)) and +1), so lane
-// l fetches row 8*(n / (DP/64)) + (l & 31)/4, logical chunk 4*sub + ((l & 3) ^ ((row>>2)&3)).
-// Rows past nrows and chunks past rowbytes read as zeros (range-checked descriptor rebuilt
-// per piece from wave-uniform values; out-of-row chunks get an out-of-range offset).
-template <int DP, int ROWS, int NT>
-struct DmaA {
-  static constexpr int NW = NT / 64;
-  static constexpr int PPRB = DP / 64;                 // pieces per 8-row block
-  static constexpr int NPIECE = ROWS * DP * 2 / 1024;
-  static constexpr int PPW = NPIECE / NW;
-  static_assert(DP % 64 == 0 && NPIECE % NW == 0 && PPW >= 1, "DMA geometry");
-  int step, bytes, w;
-  int off[PPW];
-
-  __device__ __forceinline__ void init(int step_, int nrows, int rowbytes, int gt) {
-    step = step_;
-    bytes = (int)((int64_t)(nrows - 1) * step_ + rowbytes);
-    w = __builtin_amdgcn_readfirstlane(gt >> 6);
-    const int l = gt & 63;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int n = w + NW * i;
-      const int rblk = n / PPRB, sub = 2 * (n % PPRB) + (l >> 5);
-      const int r7 = (l & 31) >> 2;
-      const int ch = 4 * sub + ((l & 3) ^ ((2 * rblk + (r7 >> 2)) & 3));
-      off[i] = ch * 16 < rowbytes ? (rblk * 8 + r7) * step + ch * 16 : 0x40000000;
-    }
-  }
-  __device__ __forceinline__ void issue(const char* head, int t, char* dst) const {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int n = w + NW * i;
-      const int rb = t * step;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(head + rb), (short)0, max(bytes - rb, 0), 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(dst + n * 1024), 16, off[i], 0, 0, 0);
-    }
-  }
-};
-
 // Row fragments of one row (16-bit, contiguous): elements d = 16*s + 8*hh + j.
 template <int DP>
 __device__ __forceinline__ void load_frags16(i16x8 (&f)[DP / 16], const uint16_t* row, bool valid,

@@ -1,0 +1,448 @@
+// attention_fwd_v2.hip — second-generation forward for 16-bit operands on gfx950.
+//
+// Same algorithm and numerics contract as attention_fwd.hip (the reference forward,
+// AttentionKernel+Source.swift:372-416: S = QK^T, base-2 online softmax, O = PV / l,
+// L = m + log2 l), restricted to fp16/bf16 Q/K/V with contiguous 16-byte aligned rows,
+// D % 8 == 0, D <= DP ∈ {64, 128, 256}, a positive softmax scale, and at most causal /
+// sliding-window masks whose fully masked tiles may be skipped (so no row is masked
+// everywhere).  The host routes everything else to the other kernels.
+//
+// What is different from attention_fwd_fast.hip, all aimed at the VALU work per MFMA (the
+// binding limit of that kernel):
+//   * K/V tiles land by LDS-DMA in the sub-tiled TileA image, so every fragment read is a base
+//     register plus an immediate (no per-read address arithmetic);
+//   * fp16: Q is pre-scaled by c = scale·log2(e) in registers and the first QK^T MFMA of each
+//     chain accumulates onto a register tile holding −m (the running row max), so the MFMA
+//     output already is S·c − m and P = exp2(S') needs no subtract or multiply per element.
+//     (bf16 keeps the fused multiply-add: pre-scaling would round Q·c to 8 bits.);
+//   * masked scores are −inf: with no fully masked row the reference's finite mask value and
+//     −inf give the same P (exactly 0) and the same O and L.
+// Lazy rescaling (threshold 8 in log2 units, cdna_hip_programming.md T13) is kept: the running
+// max and the −m tile change only when a tile's max exceeds m + 8.
+#include "mfa_stage.h"
+#include "mfa_dispatch.h"
+
+namespace mfa {
+
+// Per-wave running state of 32 query rows (one per lane, halves split the head dimension).
+template <int DP>
+struct RowState {
+  f32x16 o[DP / 32];
+  f32x16 negm;   // −moff in every register (fp16 path): the QK^T chain's initial accumulator
+  float m;       // running max (log2 units, reference convention)
+  float moff;    // the max subtracted inside S' (== m once the row has seen an unmasked key)
+  float lh;      // partial row sum of this half-wave's keys
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int dt = 0; dt < DP / 32; ++dt) o[dt] = zero16();
+    negm = zero16();
+    m = -kFltMax;
+    moff = 0.f;
+    lh = 0.f;
+  }
+};
+
+// One BK-key tile for one wave: S^T = K·Q^T (key in registers, query on the lane), masks,
+// online softmax, O^T += V^T·P^T.
+template <class E, int DP, int BK>
+__device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const int (&rbase)[2],
+                                          const int (&trb)[2], const i16x8 (&qf)[DP / 16],
+                                          RowState<DP>& st, int t, bool mask_tile, int qi,
+                                          const FwdParams& p, float c, int wsz, int hh) {
+  using A = Arith16<E, DP>;
+  constexpr bool PS = E::prec == P_FP16;  // pre-scaled Q, S' = S·c − moff from the MFMA
+  constexpr int NJ = BK / 32, DS = DP / 16, ND = DP / 32;
+  constexpr float THR = 8.0f;
+  f32x16 s[NJ];
+  {
+    constexpr int NM = DS * NJ;
+    constexpr int AH = 4;
+    i16x8 kf[AH];
+#pragma unroll
+    for (int i = 0; i < AH; ++i) kf[i] = A::read_row_a(kt, rbase, i % NJ, i / NJ);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const int ds = i / NJ, j = i % NJ;
+      if (ds == 0)
+        s[j] = A::mma(kf[i % AH], qf[0], PS ? st.negm : zero16());
+      else
+        s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
+      if (i + AH < NM) kf[i % AH] = A::read_row_a(kt, rbase, (i + AH) % NJ, (i + AH) / NJ);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  if (mask_tile) {
+    MFA_KEEP_BRANCH();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = t + j * 32 + acc_row(i, hh);
+        if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz) || key >= p.C)
+          s[j][i] = -__builtin_inff();
+      }
+  }
+
+  float mx = s[0][0];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[j][i]);
+  mx = cross_half_max(mx);
+  // Tile max in absolute log2 units.
+  const float mt = PS ? mx + st.moff : mx * c;
+  if (__any(mt > st.m + THR)) {
+    MFA_KEEP_BRANCH();
+    const float m_new = fmaxf(st.m, mt);
+    const float corr = __builtin_amdgcn_exp2f(st.m - m_new);
+    st.m = m_new;
+    st.lh *= corr;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st.o[dt][i] *= corr;
+    if constexpr (PS) {
+      // Rows still at the initial max saw only masked keys (S' = −inf): keep their offset.
+      const float moff_new = m_new > kMaskLevel ? m_new : st.moff;
+      const float shift = moff_new - st.moff;
+      st.moff = moff_new;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[j][i] -= shift;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st.negm[i] = -moff_new;
+    }
+  }
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float x = PS ? s[j][i] : __builtin_fmaf(s[j][i], c, -st.m);
+      const float pv = __builtin_amdgcn_exp2f(x);
+      s[j][i] = pv;
+      rs[i & 3] += pv;
+    }
+  st.lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
+
+  {
+    constexpr int NM = NJ * 2 * ND;
+    constexpr int AH = 3;
+    i16x8 pb[NJ * 2];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) pb[j * 2 + ks] = A::pack(s[j], ks);
+    i16x8 vf[AH];
+#pragma unroll
+    for (int i = 0; i < AH; ++i) {
+      const int jk = i / ND, dt = i % ND;
+      vf[i] = A::read_tr_a(vt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
+    }
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const int jk = i / ND, dt = i % ND;
+      st.o[dt] = A::mma(vf[i % AH], pb[jk], st.o[dt]);
+      if (i + AH < NM) {
+        const int jn = (i + AH) / ND, dn = (i + AH) % ND;
+        vf[i % AH] = A::read_tr_a(vt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// Q fragments of the lane's query row, pre-scaled by c (rounded to the element type) on the
+// fp16 path.
+template <class E, int DP>
+__device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p, int b, int h,
+                                        int qi, bool qvalid, int hh, float c) {
+  const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh +
+                         (int64_t)(qvalid ? qi : 0) * p.q.ss;
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (qvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
+    if constexpr (E::prec == P_FP16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (short)E::from_f32(E::to_f32((uint16_t)v[j]) * c);
+    }
+    qf[s] = v;
+  }
+}
+
+template <int DP>
+__device__ __forceinline__ void store_o_l(const FwdParams& p, const f32x16 (&o)[DP / 32],
+                                          float m, float l, int b, int h, int qi, int hh) {
+  const float inv = p.o_mul / l;
+  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)qi * p.o_ss;
+#pragma unroll
+  for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = dt * 32 + 8 * g + 4 * hh;
+      if (d < p.D)
+        *reinterpret_cast<float4*>(orow + d) =
+            make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
+                        o[dt][4 * g + 3] * inv);
+    }
+  if (hh == 0) {
+    const float L = m + __log2f(l);
+    const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
+    if (p.l_f16)
+      reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+    else
+      reinterpret_cast<float*>(p.l)[li] = L;
+  }
+}
+
+__device__ __forceinline__ void key_range(const FwdParams& p, int q0, int BQ, int BK, int* kbeg,
+                                          int* kend) {
+  *kend = p.C;
+  if (p.mask.causal) *kend = min(*kend, q0 + BQ);
+  *kbeg = 0;
+  if (p.mask.window) {
+    const int64_t lo = (int64_t)q0 - (int64_t)p.mask.window_size;
+    *kbeg = lo > 0 ? (int)(lo / BK) * BK : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// One 128-row query block per workgroup (4 waves x 32 rows); WPS workgroups' waves per SIMD.
+template <class E, int DP, int BK, int WPS>
+__global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
+  constexpr int NT = 256, BQ = 128;
+  constexpr int TILEB = BK * DP * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const kb0 = smem;
+  char* const vb0 = smem + 2 * TILEB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
+  const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
+  const int BH = p.B * p.H;
+  const int bid = blockIdx.x;
+  const int rb = p.nblk - 1 - bid / BH;  // heaviest causal blocks first
+  const int bh = bid % BH;
+  const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
+  const int q0 = rb * BQ;
+  const int qi = q0 + wave * 32 + l32;
+  const bool qvalid = qi < p.R;
+  const float c = p.c_log2;
+  const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+
+  int kbeg, kend;
+  key_range(p, q0, BQ, BK, &kbeg, &kend);
+  DmaA<DP, BK, NT> kd, vd;
+  kd.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
+  vd.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
+  const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
+  const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
+  if (kbeg < kend) {
+    kd.issue(khead, kbeg, kb0);
+    vd.issue(vhead, kbeg, vb0);
+  }
+  i16x8 qf[DP / 16];
+  load_q2<E, DP>(qf, p, b, h, qi, qvalid, hh, c);
+  RowState<DP> st;
+  st.init();
+  wait_vm();
+  __syncthreads();
+
+  int cur = 0;
+  for (int t = kbeg; t < kend; t += BK) {
+    if (t + BK < kend) {
+      kd.issue(khead, t + BK, kb0 + (cur ^ 1) * TILEB);
+      vd.issue(vhead, t + BK, vb0 + (cur ^ 1) * TILEB);
+    }
+    const bool mask_tile = (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
+    fwd2_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t, mask_tile,
+                         qi, p, c, wsz, hh);
+    wait_vm();
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float l = cross_half_sum(st.lh) + kFltMin;
+  if (!(l > 0.f)) l = kFltMin;
+  if (qvalid) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+}
+
+// ---------------------------------------------------------------------------------------
+// Causal balance: 8 waves = two groups of 4.  A workgroup owns the mirrored pair of query
+// blocks (i, nblk-1-i) (equal causal work per workgroup); inside each block group 0 takes
+// the first half of the key tiles and group 1 the second half, and the two partial softmax
+// states (O, m, l) merge through LDS before group 0 stores the block.
+template <class E, int DP, int BK>
+__global__ void __launch_bounds__(512, 2) mfa_fwd2_pair_kernel(FwdParams p) {
+  constexpr int NT = 256, BQ = 128, ND = DP / 32;
+  constexpr int TILEB = BK * DP * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gt = tid & 255;
+  const int lane = tid & 63, wg = gt >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
+  const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
+  char* const kb0 = smem + g * 4 * TILEB;
+  char* const vb0 = kb0 + 2 * TILEB;
+
+  const int BH = p.B * p.H;
+  const int bid = blockIdx.x;
+  const int pi = bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
+  const float c = p.c_log2;
+  const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+
+  DmaA<DP, BK, NT> kd, vd;
+  kd.init((int)p.k.ss * 2, p.C, p.D * 2, gt);
+  vd.init((int)p.v.ss * 2, p.C, p.D * 2, gt);
+  const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
+  const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
+
+  const int rbA = pi, rbB = p.nblk - 1 - pi;
+  for (int which = 0; which < 2; ++which) {
+    const int rb = which == 0 ? rbB : rbA;
+    if (which == 1 && rbA >= rbB) break;  // odd middle block handled once
+    const int q0 = rb * BQ;
+    const int qi = q0 + wg * 32 + l32;
+    const bool qvalid = qi < p.R;
+    int kbeg, kend;
+    key_range(p, q0, BQ, BK, &kbeg, &kend);
+    const int ntile = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    const int nA = (ntile + 1) / 2;
+    const int t0 = g == 0 ? kbeg : kbeg + nA * BK;
+    const int t1 = g == 0 ? min(kend, kbeg + nA * BK) : kend;
+
+    if (t0 < t1) {
+      kd.issue(khead, t0, kb0);
+      vd.issue(vhead, t0, vb0);
+    }
+    i16x8 qf[DP / 16];
+    load_q2<E, DP>(qf, p, b, h, qi, qvalid, hh, c);
+    RowState<DP> st;
+    st.init();
+    wait_vm();
+    __syncthreads();
+    int cur = 0;
+    for (int step = 0; step < nA; ++step) {
+      const int t = t0 + step * BK;
+      if (t < t1) {
+        if (t + BK < t1) {
+          kd.issue(khead, t + BK, kb0 + (cur ^ 1) * TILEB);
+          vd.issue(vhead, t + BK, vb0 + (cur ^ 1) * TILEB);
+        }
+        const bool mask_tile =
+            (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
+        fwd2_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t,
+                             mask_tile, qi, p, c, wsz, hh);
+        wait_vm();
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+
+    // Merge group 1's partial state into group 0 through LDS (the staging ring is free).
+    float* mrg = reinterpret_cast<float*>(smem);        // [4 waves][ND*16][64]
+    float* mml = mrg + 4 * ND * 16 * 64;                // [4 waves][2][64]
+    if (g == 1) {
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mrg[((wg * ND + dt) * 16 + i) * 64 + lane] = st.o[dt][i];
+      mml[(wg * 2 + 0) * 64 + lane] = st.m;
+      mml[(wg * 2 + 1) * 64 + lane] = st.lh;
+    }
+    __syncthreads();
+    if (g == 0) {
+      const float mb = mml[(wg * 2 + 0) * 64 + lane];
+      const float lb = mml[(wg * 2 + 1) * 64 + lane];
+      const float mf = fmaxf(st.m, mb);
+      const float ca = __builtin_amdgcn_exp2f(st.m - mf);
+      const float cb = __builtin_amdgcn_exp2f(mb - mf);
+      float l = cross_half_sum(st.lh * ca + lb * cb) + kFltMin;
+      if (!(l > 0.f)) l = kFltMin;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          st.o[dt][i] = st.o[dt][i] * ca + mrg[((wg * ND + dt) * 16 + i) * 64 + lane] * cb;
+      if (qvalid) store_o_l<DP>(p, st.o, mf, l, b, h, qi, hh);
+    }
+    __syncthreads();
+  }
+}
+
+template <class E, int DP, int BK, int WPS>
+static hipError_t launch_fwd2(const FwdParams& p, hipStream_t stream) {
+  constexpr int LDS = 4 * BK * DP * 2;
+  auto kern = mfa_fwd2_kernel<E, DP, BK, WPS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
+  return hipGetLastError();
+}
+
+template <class E, int DP, int BK>
+static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
+  constexpr int LDS = 8 * BK * DP * 2;
+  static_assert(LDS >= 4 * (DP / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4, "merge area");
+  auto kern = mfa_fwd2_pair_kernel<E, DP, BK>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int npairs = (p.nblk + 1) / 2;
+  hipLaunchKernelGGL(kern, dim3(npairs * p.B * p.H), dim3(512), LDS, stream, p);
+  return hipGetLastError();
+}
+
+// hipErrorNotSupported when the configuration is not covered (the caller falls back).
+hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
+  const char* var = getenv("MFA_FWD_VARIANT");
+  const int blocks = p.nblk * p.B * p.H;
+  bool single = !p.mask.causal || blocks > 768 || DP > 128;
+  if (var && var[0] == 's') single = true;
+  if (var && var[0] == 'p') single = false;
+#define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                  \
+  if (elem == ELEM && DP == DPV)                                        \
+    return single ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)           \
+                  : launch_fwd2_pair<EE, DPV, BKV>(p, stream);
+  MFA_F2(P_FP16, F16, 64, 64, 2)
+  MFA_F2(P_FP16, F16, 128, 64, 2)
+  MFA_F2(P_BF16, BF16, 64, 64, 2)
+  MFA_F2(P_BF16, BF16, 128, 64, 2)
+#undef MFA_F2
+  if (elem == P_FP16 && DP == 256) return launch_fwd2<F16, 256, 32, 1>(p, stream);
+  if (elem == P_BF16 && DP == 256) return launch_fwd2<BF16, 256, 32, 1>(p, stream);
+  return hipErrorNotSupported;
+}
+
+#define MFA_F2_INST(EE, DPV, BKV, WPS)                                        \
+  template __global__ void mfa_fwd2_kernel<EE, DPV, BKV, WPS>(FwdParams);     \
+  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV>(FwdParams);
+MFA_F2_INST(F16, 64, 64, 2)
+MFA_F2_INST(F16, 128, 64, 2)
+MFA_F2_INST(BF16, 64, 64, 2)
+MFA_F2_INST(BF16, 128, 64, 2)
+#undef MFA_F2_INST
+template __global__ void mfa_fwd2_kernel<F16, 256, 32, 1>(FwdParams);
+template __global__ void mfa_fwd2_kernel<BF16, 256, 32, 1>(FwdParams);
+
+}  // namespace mfa

@@ -219,7 +219,35 @@ bool fast_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
   return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1;
 }
 
+// attention_fwd_v2.hip: also D = 256, but needs a positive scale and, with causal / window
+// masks, no fully masked row (skip_ok), since it masks with -inf.
+bool fwd2_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
+  if (const char* e = getenv("MFA_FWD_GEN")) {
+    if (e[0] == '1') return false;
+  }
+  if (elem != 1 && elem != 2) return false;
+  if (kvsrc != 0 || (DP != 64 && DP != 128 && DP != 256)) return false;
+  if (!(p.c_log2 > 0.f)) return false;
+  if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok) return false;
+  if (p.D % 8 != 0 || p.mask.amask || p.mask.ranges) return false;
+  if (!p.q.vec || !p.k.vec || !p.v.vec) return false;
+  const int prec = elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16;
+  if (p.q.prec != prec || p.k.prec != prec || p.v.prec != prec) return false;
+  if (p.k.bscale || p.v.bscale) return false;
+  if ((int64_t)p.C * p.k.ss * 2 >= ((int64_t)1 << 31) ||
+      (int64_t)p.C * p.v.ss * 2 >= ((int64_t)1 << 31))
+    return false;
+  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1;
+}
+
 hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, hipStream_t s) {
+  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+    if (e[0] == '1') return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
+  }
+  if (fwd2_eligible(p, elem, DP, kvsrc)) {
+    hipError_t e = mfa::fwd2_dispatch(p, elem, DP, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (fast_eligible(p, elem, DP, kvsrc)) {
     const char* var = getenv("MFA_FWD_VARIANT");
     if (kvsrc == 0 && DP == 128 && var && var[0] == 'w') {

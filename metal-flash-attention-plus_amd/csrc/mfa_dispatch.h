@@ -50,6 +50,8 @@ hipError_t bwd_kv_dispatch(const BwdParams& p, int elem, int DP, int ksrc, int v
 int bwd_lds_bytes(int kind, int elem, int DP);
 // Tuned 16-bit backward phases (attention_bwd_fast.hip); kind 0 = query, 1 = key/value.
 hipError_t bwd_fast_dispatch(const BwdParams& p, int kind, int elem, int DP, hipStream_t stream);
+// Second-generation 16-bit forward (attention_fwd_v2.hip).
+hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 hipError_t fwd_fast_dispatch(const FwdParams& p, int elem, int DP, int kvsrc, hipStream_t stream);
 // One-wave-per-SIMD forward with two query blocks per wave (attention_fwd_wide.hip).
 hipError_t fwd_wide_dispatch(const FwdParams& p, int elem, hipStream_t stream);
