@@ -31,8 +31,8 @@ PEAK_INT8_TOPS = 2 * PEAK_FP16_TFLOPS
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--heads", type=int, default=16)
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--dim", type=int, default=128)

@@ -85,10 +85,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
   const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
-  const int BH = p.B * p.H;
-  const int bid = blockIdx.x;
-  const int rb = p.nblk - 1 - bid / BH;
-  const int bh = bid % BH;
+  int bh, blk;
+  xcd_unit_block(blockIdx.x, p.B * p.H, p.nblk, &bh, &blk);
+  const int rb = p.nblk - 1 - blk;  // heaviest causal blocks first
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const int q0 = rb * BQ;
   const int qi = q0 + wave * 32 + l32;
@@ -259,10 +258,8 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
   const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
-  const int BH = p.B * p.Hkv;
-  const int bid = blockIdx.x;
-  const int kb = bid / BH;
-  const int bh = bid % BH;
+  int bh, kb;
+  xcd_unit_block(blockIdx.x, p.B * p.Hkv, p.nblk, &bh, &kb);
   const int b = bh / p.Hkv, kvh = bh % p.Hkv;
   const int k0 = kb * BK;
   const int ki = k0 + wave * 32 + l32;

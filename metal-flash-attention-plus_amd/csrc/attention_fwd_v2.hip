@@ -15,6 +15,9 @@
 //     chain accumulates onto a register tile holding −m (the running row max), so the MFMA
 //     output already is S·c − m and P = exp2(S') needs no subtract or multiply per element.
 //     (bf16 keeps the fused multiply-add: pre-scaling would round Q·c to 8 bits.);
+//   * built with MFMA accumulators in VGPRs (Makefile): the in-loop O rescale would otherwise
+//     make hipcc copy all of O between AGPRs and VGPRs every iteration; D=256 then fits in
+//     244 registers and runs two waves per SIMD;
 //   * masked scores are −inf: with no fully masked row the reference's finite mask value and
 //     −inf give the same P (exactly 0) and the same O and L.
 // Lazy rescaling (threshold 8 in log2 units, cdna_hip_programming.md T13) is kept: the running
@@ -50,13 +53,15 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
                                           RowState<DP>& st, int t, bool mask_tile, int qi,
                                           const FwdParams& p, float c, int wsz, int hh) {
   using A = Arith16<E, DP>;
-  constexpr bool PS = E::prec == P_FP16;  // pre-scaled Q, S' = S·c − moff from the MFMA
+  // Pre-scaled Q, S' = S·c − moff from the MFMA (fp16 up to D=128: at D=256 the −m tile's
+  // registers are worth more than the per-element multiply-add, which halves per MFMA there).
+  constexpr bool PS = E::prec == P_FP16 && DP <= 128;
   constexpr int NJ = BK / 32, DS = DP / 16, ND = DP / 32;
   constexpr float THR = 8.0f;
   f32x16 s[NJ];
   {
     constexpr int NM = DS * NJ;
-    constexpr int AH = 4;
+    constexpr int AH = DP > 128 ? 2 : 4;
     i16x8 kf[AH];
 #pragma unroll
     for (int i = 0; i < AH; ++i) kf[i] = A::read_row_a(kt, rbase, i % NJ, i / NJ);
@@ -129,7 +134,7 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
 
   {
     constexpr int NM = NJ * 2 * ND;
-    constexpr int AH = 3;
+    constexpr int AH = DP > 128 ? 2 : 3;
     i16x8 pb[NJ * 2];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -166,7 +171,7 @@ __device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p
     const int d0 = 16 * s + 8 * hh;
     i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (qvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-    if constexpr (E::prec == P_FP16) {
+    if constexpr (E::prec == P_FP16 && DP <= 128) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (short)E::from_f32(E::to_f32((uint16_t)v[j]) * c);
     }
@@ -225,10 +230,16 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
   const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
-  const int BH = p.B * p.H;
-  const int bid = blockIdx.x;
-  const int rb = p.nblk - 1 - bid / BH;  // heaviest causal blocks first
-  const int bh = bid % BH;
+  // Causal: heaviest blocks first over the whole grid (balance); otherwise each head's blocks
+  // together on one XCD (L2 reuse of its K/V).
+  int bh, blk;
+  if (p.mask.causal) {
+    bh = blockIdx.x % (p.B * p.H);
+    blk = blockIdx.x / (p.B * p.H);
+  } else {
+    xcd_unit_block(blockIdx.x, p.B * p.H, p.nblk, &bh, &blk);
+  }
+  const int rb = p.nblk - 1 - blk;
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const int q0 = rb * BQ;
   const int qi = q0 + wave * 32 + l32;
@@ -429,8 +440,8 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   MFA_F2(P_BF16, BF16, 64, 64, 2)
   MFA_F2(P_BF16, BF16, 128, 64, 2)
 #undef MFA_F2
-  if (elem == P_FP16 && DP == 256) return launch_fwd2<F16, 256, 32, 1>(p, stream);
-  if (elem == P_BF16 && DP == 256) return launch_fwd2<BF16, 256, 32, 1>(p, stream);
+  if (elem == P_FP16 && DP == 256) return launch_fwd2<F16, 256, 32, 2>(p, stream);
+  if (elem == P_BF16 && DP == 256) return launch_fwd2<BF16, 256, 32, 2>(p, stream);
   return hipErrorNotSupported;
 }
 
@@ -442,7 +453,7 @@ MFA_F2_INST(F16, 128, 64, 2)
 MFA_F2_INST(BF16, 64, 64, 2)
 MFA_F2_INST(BF16, 128, 64, 2)
 #undef MFA_F2_INST
-template __global__ void mfa_fwd2_kernel<F16, 256, 32, 1>(FwdParams);
-template __global__ void mfa_fwd2_kernel<BF16, 256, 32, 1>(FwdParams);
+template __global__ void mfa_fwd2_kernel<F16, 256, 32, 2>(FwdParams);
+template __global__ void mfa_fwd2_kernel<BF16, 256, 32, 2>(FwdParams);
 
 }  // namespace mfa

@@ -269,6 +269,23 @@ __device__ __forceinline__ float mul_rn(float a, float b) {
 // it the compiler if-converts the body into per-element selects that then run on every tile.
 #define MFA_KEEP_BRANCH() asm volatile("" ::: "memory")
 
+// Workgroup -> (unit, block) map that keeps each unit's blocks on one XCD, in order
+// (cdna_hip_programming.md T1).  Workgroups are dealt round-robin over the 8 XCDs, so with
+// units % 8 == 0 the XCD that receives workgroups x, x+8, x+16, ... walks the blocks of units
+// x, x+8, ... one unit at a time: the unit's shared operands (K/V of a head in the forward,
+// Q/dO or K/V in the backward) stay in that XCD's L2.  Placement only changes speed.
+__device__ __forceinline__ void xcd_unit_block(int bid, int units, int nblk, int* unit,
+                                               int* blk) {
+  if ((units & 7) == 0) {
+    const int j = bid >> 3;
+    *unit = (j / nblk) * 8 + (bid & 7);
+    *blk = j % nblk;
+  } else {
+    *unit = bid % units;
+    *blk = bid / units;
+  }
+}
+
 // Row index (within a 32-row MFMA output tile) of accumulator register i in lane half h.
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
