@@ -326,4 +326,9 @@ hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) 
   return hipErrorNotSupported;
 }
 
+// Explicit instantiations (hipcc does not always emit the host-side stubs of kernel templates
+// that are only named through a launch helper).
+template __global__ void mfa_fwd_i8_kernel<F16, 128, 64, 3>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<BF16, 128, 64, 3>(FwdParams);
+
 }  // namespace mfa
