@@ -9,7 +9,9 @@
 // wave held in registers for the whole kernel; the traversed operand pair streams through a
 // double-buffered LDS ring filled by LDS-DMA (buffer_load ... lds, no staging registers), one
 // barrier per tile.  Fragment reads are issued a few MFMAs ahead of their use and the order is
-// pinned with sched_barrier (left alone, hipcc issues each read right before its MFMA).
+// pinned with sched_barrier (left alone, hipcc issues each read right before its MFMA).  With
+// one wave per SIMD nothing else hides the softmax, so its VALU work is threaded between the
+// MFMAs of the next product that does not depend on it (exp under dP, dS under dV or dQ).
 //
 //   bwd_q  (3 GEMMs): S^T = K·Q^T, dP^T = V·dO^T (query on the lane), P^T = exp2(S^T·c − L),
 //                     dS^T = P^T∘(dP^T·scale − D), dQ^T += K^T·dS^T.  Writes D.
@@ -65,6 +67,53 @@ __device__ __forceinline__ void dual_rows_chain(const char* t1, const char* t2,
     else
       acc1[j] = A::mma(fr[i % AH], b1[ds], acc1[j]);
     if (i + AH < NM) fr[i % AH] = rd(i + AH);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// acc[j] += A(rows j*32.. of an LDS row tile, k-step ds) · b[ds] over all (ds, j), fragment
+// reads AH MFMAs ahead, order pinned; after MFMA i the hook runs VALU slice i, so work that
+// does not feed this chain (the previous product's softmax) issues between its MFMAs.
+template <class A, int NJ, class Hook>
+__device__ __forceinline__ void rows_chain(const char* tile, const i16x8* b, f32x16 (&acc)[NJ],
+                                           const int (&rbase)[2], Hook&& hook) {
+  constexpr int NM = A::DSTEPS * NJ;
+  constexpr int AH = A::DSTEPS >= 16 ? 2 : 4;  // D=256 runs at the 512-register limit
+  i16x8 fr[AH];
+#pragma unroll
+  for (int i = 0; i < AH; ++i) fr[i] = A::read_row_a(tile, rbase, i % NJ, i / NJ);
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const int ds = i / NJ, j = i % NJ;
+    acc[j] = A::mma(fr[i % AH], b[ds], acc[j]);
+    if (i + AH < NM) fr[i % AH] = A::read_row_a(tile, rbase, (i + AH) % NJ, (i + AH) / NJ);
+    hook(i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// acc[dt] += A^T(transposed reads of an LDS row tile) · b[jk] over (jk, dt), jk = 32-row
+// sub-tile x k-step; hook(i) after MFMA i as above.
+template <class A, int NJ, int ND, class Hook>
+__device__ __forceinline__ void tr_chain(const char* tile, const int (&trb)[2], const i16x8* b,
+                                         f32x16 (&acc)[ND], Hook&& hook) {
+  constexpr int NM = NJ * 2 * ND;
+  constexpr int AH = ND >= 8 ? 2 : 3;
+  i16x8 fr[AH];
+#pragma unroll
+  for (int i = 0; i < AH; ++i) {
+    const int jk = i / ND, dt = i % ND;
+    fr[i] = A::read_tr_a(tile, trb, (jk >> 1) * 32, jk & 1, dt * 32);
+  }
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const int jk = i / ND, dt = i % ND;
+    acc[dt] = A::mma(fr[i % AH], b[jk], acc[dt]);
+    if (i + AH < NM) {
+      const int jn = (i + AH) / ND, dn = (i + AH) % ND;
+      fr[i % AH] = A::read_tr_a(tile, trb, (jn >> 1) * 32, jn & 1, dn * 32);
+    }
+    hook(i);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -168,11 +217,13 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     }
     const char* kt = kb0 + cur * TILEB;
     const char* vt = vb0 + cur * TILEB;
+    // S^T = K·Q^T; masks; dP^T = V·dO^T with P^T = exp2(S^T·c − L) computed between its
+    // MFMAs; dQ^T += K^T·dS^T with each k-step's dS^T = P^T∘(dP^T·scale − D) computed under
+    // the previous k-step's MFMAs.
     f32x16 s[NJ], dp[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) { s[j] = zero16(); dp[j] = zero16(); }
-    dual_rows_chain<A, NJ>(kt, vt, qf, dof, s, dp, rbase);
-
+    rows_chain<A, NJ>(kt, qf, s, rbase, [](int) {});
     const bool diag = (p.mask.causal && t + BT - 1 > q0) || p.mask.window;
     if (diag) {
       MFA_KEEP_BRANCH();
@@ -184,39 +235,40 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
           if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) s[j][i] = kMaskValue;
         }
     }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -Lrow));
-        dp[j][i] = pv * __builtin_fmaf(dp[j][i], sc, -Drow);
-      }
-
-    // dQ^T += K^T · dS^T (K^T by transposed reads), reads AH MFMAs ahead.
     {
-      constexpr int NM = NJ * 2 * ND;
-      constexpr int AH = 3;
-      i16x8 sb[NJ * 2];
+      constexpr int EPM = 16 / DS;  // P elements per dP MFMA (NJ*16 over DS*NJ MFMAs)
+      rows_chain<A, NJ>(vt, dof, dp, rbase, [&](int i) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) sb[j * 2 + ks] = A::pack(dp[j], ks);
-      i16x8 kf[AH];
-#pragma unroll
-      for (int i = 0; i < AH; ++i) {
-        const int jk = i / ND, dt = i % ND;
-        kf[i] = A::read_tr_a(kt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
-      }
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        const int jk = i / ND, dt = i % ND;
-        dq[dt] = A::mma(kf[i % AH], sb[jk], dq[dt]);
-        if (i + AH < NM) {
-          const int jn = (i + AH) / ND, dn = (i + AH) % ND;
-          kf[i % AH] = A::read_tr_a(kt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
+        for (int e = 0; e < EPM; ++e) {
+          const int idx = i * EPM + e, jj = idx >> 4, ii = idx & 15;
+          s[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -Lrow));
         }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      });
+    }
+    {
+      // dS^T of k-step jk = registers 8*(jk&1)..+7 of sub-tile jk>>1, packed as the B operand.
+      i16x8 sb[NJ * 2];
+      auto ds_step = [&](int jk) {
+        const int j = jk >> 1, base = 8 * (jk & 1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          dp[j][base + e] = s[j][base + e] * __builtin_fmaf(dp[j][base + e], sc, -Drow);
+        sb[jk] = A::pack(dp[j], jk & 1);
+      };
+      ds_step(0);
+      constexpr int EPM = 8 / ND;  // dS elements per dQ MFMA: next k-step's 8 over ND MFMAs
+      tr_chain<A, NJ, ND>(kt, trb, sb, dq, [&](int i) {
+        const int jk = i / ND, r = i % ND;
+        if (jk + 1 < NJ * 2) {
+          const int jn = jk + 1, j = jn >> 1, base = 8 * (jn & 1);
+#pragma unroll
+          for (int e = 0; e < EPM; ++e) {
+            const int el = base + r * EPM + e;
+            dp[j][el] = s[j][el] * __builtin_fmaf(dp[j][el], sc, -Drow);
+          }
+          if (r == ND - 1) sb[jn] = A::pack(dp[j], jn & 1);
+        }
+      });
     }
     wait_vm();
     __syncthreads();
@@ -353,39 +405,80 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     f32x16 s[NJ], dp[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) { s[j] = zero16(); dp[j] = zero16(); }
-    dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase);
-
-    const bool diag = (p.mask.causal && k0 + BK - 1 > t) || p.mask.window;
-    if (diag) {
-      MFA_KEEP_BRANCH();
+    // L and D of accumulator row (j, i) = query j*32 + 8*(i>>2) + 4*hh + (i&3).
+    auto lds4 = [&](const float* base, float (&v)[NJ][16]) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 x = *reinterpret_cast<const float4*>(base + j * 32 + 8 * g4 + 4 * hh);
+          v[j][4 * g4] = x.x; v[j][4 * g4 + 1] = x.y; v[j][4 * g4 + 2] = x.z; v[j][4 * g4 + 3] = x.w;
+        }
+    };
+    auto apply_mask = [&]() {
+      if ((p.mask.causal && k0 + BK - 1 > t) || p.mask.window) {
+        MFA_KEEP_BRANCH();
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int q = t + j * 32 + acc_row(i, hh);
+            if ((p.mask.causal && ki > q) || (p.mask.window && q - ki > wsz)) s[j][i] = kMaskValue;
+          }
+      }
+    };
+    if constexpr (DP <= 128) {
+      // S = Q·K^T; masks; dP = dO·V^T with P = exp2(S·c − L) computed between its MFMAs;
+      // dV^T += dO^T·P with dS = P∘(dP·scale − D) computed between its MFMAs; dK^T += Q^T·dS.
+      rows_chain<A, NJ>(qt, kf, s, rbase, [](int) {});
+      apply_mask();
+      {
+        float lv[NJ][16];
+        lds4(lt, lv);
+        constexpr int EPM = 16 / DS;
+        rows_chain<A, NJ>(ot, vf, dp, rbase, [&](int i) {
+#pragma unroll
+          for (int e = 0; e < EPM; ++e) {
+            const int idx = i * EPM + e, jj = idx >> 4, ii = idx & 15;
+            s[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -lv[jj][ii]));
+          }
+        });
+      }
+      i16x8 pb[NJ * 2], sb[NJ * 2];
+#pragma unroll
+      for (int jk = 0; jk < NJ * 2; ++jk) pb[jk] = A::pack(s[jk >> 1], jk & 1);
+      float dv_[NJ][16];
+      lds4(dtl, dv_);
+      constexpr int NMV = NJ * 2 * ND;
+      constexpr int EPM = (NJ * 16 + NMV - 1) / NMV;
+      tr_chain<A, NJ, ND>(ot, trb, pb, dv, [&](int i) {
+#pragma unroll
+        for (int e = 0; e < EPM; ++e) {
+          const int idx = i * EPM + e;
+          if (idx < NJ * 16) {
+            const int jj = idx >> 4, ii = idx & 15;
+            dp[jj][ii] = s[jj][ii] * __builtin_fmaf(dp[jj][ii], sc, -dv_[jj][ii]);
+            if ((ii & 7) == 7) sb[jj * 2 + (ii >> 3)] = A::pack(dp[jj], ii >> 3);
+          }
+        }
+      });
+      tr_chain<A, NJ, ND>(qt, trb, sb, dk, [](int) {});
+    } else {
+      // D = 256 runs at the register limit: S and dP chains together, then the softmax, then
+      // dV and dK together.
+      dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase);
+      apply_mask();
+      float lv[NJ][16], dv_[NJ][16];
+      lds4(lt, lv);
+      lds4(dtl, dv_);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int q = t + j * 32 + acc_row(i, hh);
-          if ((p.mask.causal && ki > q) || (p.mask.window && q - ki > wsz)) s[j][i] = kMaskValue;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int r0 = j * 32 + 8 * g4 + 4 * hh;
-        const float4 l4 = *reinterpret_cast<const float4*>(lt + r0);
-        const float4 d4 = *reinterpret_cast<const float4*>(dtl + r0);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-        const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -lv[e]));
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -lv[j][i]));
           s[j][i] = pv;
-          dp[j][i] = pv * __builtin_fmaf(dp[j][i], sc, -dv4[e]);
+          dp[j][i] = pv * __builtin_fmaf(dp[j][i], sc, -dv_[j][i]);
         }
-      }
-
-    // dV^T += dO^T · P and dK^T += Q^T · dS (transposed reads of the row tiles).
-    {
       constexpr int NM = NJ * 2 * ND * 2;
       constexpr int AH = 4;
       i16x8 pb[NJ * 2], sb[NJ * 2];

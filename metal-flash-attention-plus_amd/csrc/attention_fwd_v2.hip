@@ -27,6 +27,15 @@
 
 namespace mfa {
 
+// Scheduling knobs (development A/B; the defaults are the shipped configuration): fragment
+// read-ahead for the QK^T and PV chains, MFMA-cluster priority, order pinning.
+template <int AHK_ = 4, int AHV_ = 3, bool PRIO_ = false, bool PIN_ = true>
+struct Tune {
+  static constexpr int AHK = AHK_, AHV = AHV_;
+  static constexpr bool PRIO = PRIO_, PIN = PIN_;
+};
+using TuneDefault = Tune<>;
+
 // Per-wave running state of 32 query rows (one per lane, halves split the head dimension).
 template <int DP>
 struct RowState {
@@ -47,7 +56,7 @@ struct RowState {
 
 // One BK-key tile for one wave: S^T = K·Q^T (key in registers, query on the lane), masks,
 // online softmax, O^T += V^T·P^T.
-template <class E, int DP, int BK>
+template <class E, int DP, int BK, class TU = TuneDefault>
 __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const int (&rbase)[2],
                                           const int (&trb)[2], const i16x8 (&qf)[DP / 16],
                                           RowState<DP>& st, int t, bool mask_tile, int qi,
@@ -61,10 +70,11 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
   f32x16 s[NJ];
   {
     constexpr int NM = DS * NJ;
-    constexpr int AH = DP > 128 ? 2 : 4;
+    constexpr int AH = DP > 128 ? 2 : TU::AHK;
     i16x8 kf[AH];
 #pragma unroll
     for (int i = 0; i < AH; ++i) kf[i] = A::read_row_a(kt, rbase, i % NJ, i / NJ);
+    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const int ds = i / NJ, j = i % NJ;
@@ -73,8 +83,9 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
       else
         s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
       if (i + AH < NM) kf[i % AH] = A::read_row_a(kt, rbase, (i + AH) % NJ, (i + AH) / NJ);
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
   if (mask_tile) {
@@ -134,7 +145,7 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
 
   {
     constexpr int NM = NJ * 2 * ND;
-    constexpr int AH = DP > 128 ? 2 : 3;
+    constexpr int AH = DP > 128 ? 2 : TU::AHV;
     i16x8 pb[NJ * 2];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -146,6 +157,7 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
       const int jk = i / ND, dt = i % ND;
       vf[i] = A::read_tr_a(vt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
     }
+    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const int jk = i / ND, dt = i % ND;
@@ -154,8 +166,9 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
         const int jn = (i + AH) / ND, dn = (i + AH) % ND;
         vf[i % AH] = A::read_tr_a(vt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -217,7 +230,7 @@ __device__ __forceinline__ void key_range(const FwdParams& p, int q0, int BQ, in
 
 // ---------------------------------------------------------------------------------------
 // One 128-row query block per workgroup (4 waves x 32 rows); WPS workgroups' waves per SIMD.
-template <class E, int DP, int BK, int WPS>
+template <class E, int DP, int BK, int WPS, class TU = TuneDefault>
 __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   constexpr int NT = 256, BQ = 128;
   constexpr int TILEB = BK * DP * 2;
@@ -272,7 +285,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
       vd.issue(vhead, t + BK, vb0 + (cur ^ 1) * TILEB);
     }
     const bool mask_tile = (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
-    fwd2_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t, mask_tile,
+    fwd2_tile<E, DP, BK, TU>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t, mask_tile,
                          qi, p, c, wsz, hh);
     wait_vm();
     __syncthreads();
@@ -392,10 +405,10 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_pair_kernel(FwdParams p) {
   }
 }
 
-template <class E, int DP, int BK, int WPS>
+template <class E, int DP, int BK, int WPS, class TU = TuneDefault>
 static hipError_t launch_fwd2(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 4 * BK * DP * 2;
-  auto kern = mfa_fwd2_kernel<E, DP, BK, WPS>;
+  auto kern = mfa_fwd2_kernel<E, DP, BK, WPS, TU>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -431,6 +444,19 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   bool single = !p.mask.causal || blocks > 768 || DP > 128;
   if (var && var[0] == 's') single = true;
   if (var && var[0] == 'p') single = false;
+  // Development A/B of the scheduling knobs on the fp16 D=128 single-block kernel.
+  if (const char* tv = getenv("MFA_FWD2_TUNE")) {
+    if (elem == P_FP16 && DP == 128 && single) {
+      switch (tv[0]) {
+        case '1': return launch_fwd2<F16, 128, 64, 2, Tune<8, 4>>(p, stream);
+        case '2': return launch_fwd2<F16, 128, 64, 2, Tune<4, 3, false, false>>(p, stream);
+        case '3': return launch_fwd2<F16, 128, 64, 2, Tune<4, 3, true, true>>(p, stream);
+        case '4': return launch_fwd2<F16, 128, 128, 2>(p, stream);
+        case '5': return launch_fwd2<F16, 128, 64, 2, Tune<2, 2>>(p, stream);
+        default: break;
+      }
+    }
+  }
 #define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                  \
   if (elem == ELEM && DP == DPV)                                        \
     return single ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)           \

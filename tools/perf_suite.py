@@ -23,7 +23,7 @@ PEAK = 256 * 4 * 1024 * 2.4e9 / 1e12
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C2,C3,C4,C5")
+    ap.add_argument("--only", default="C2,C3,C4,C5,BWD128")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--c5-batch", type=int, default=8)
     args = ap.parse_args()
@@ -79,6 +79,26 @@ def main():
         emit("C2-noncausal", ms=round(ms, 4), tflops=round(f / ms / 1e9, 1))
         del q, k, v, o, l
 
+    if "TUNE" in only:
+        # A/B of attention_fwd_v2.hip scheduling knobs (MFA_FWD2_TUNE), interleaved rounds.
+        B, H, S, D = 1, 16, 8192, 128
+        q, k, v = (uni((B, H, S, D), torch.float16) for _ in range(3))
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+        f = mfa.attention_flops(B, H, S, S, D)
+        res = {}
+        for rnd in range(3):
+            for tv in "012345":
+                os.environ["MFA_FWD2_TUNE"] = tv
+                ms = time_it(lambda: mha.forward(desc, q, k, v, o, l, stream=stream), args.reps)
+                res.setdefault(tv, []).append(round(f / ms / 1e9, 1))
+        os.environ.pop("MFA_FWD2_TUNE", None)
+        for tv, r in res.items():
+            emit("TUNE", variant=tv, tflops=r)
+        del q, k, v, o, l
+
     if "C3" in only:
         B, H, S, D = 1, 16, 8192, 128
         qf = uni((B, H, S, D), torch.float16)
@@ -125,8 +145,11 @@ def main():
              frac=round(f / ms / 1e9 / PEAK, 4))
         del lat, wk, wv, q, o, kb, vb
 
-    if "C5" in only:
-        B, H, S, D = args.c5_batch, 32, 4096, 256
+    for tag, D5 in (("C5", 256), ("BWD128", 128)):
+      if tag not in only:
+        continue
+      if True:
+        B, H, S, D = args.c5_batch, 32, 4096, D5
         q, k, v, do = (uni((B, H, S, D), torch.float16) for _ in range(4))
         o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
         l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
@@ -142,7 +165,7 @@ def main():
                                             stream=stream, phase="query"), reps)
         ms_kv = time_it(lambda: mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf,
                                              stream=stream, phase="keyValue"), reps)
-        emit("C5", batch=B, fwd_ms=round(ms_f, 3), fwd_tflops=round(ff / ms_f / 1e9, 1),
+        emit(tag, batch=B, fwd_ms=round(ms_f, 3), fwd_tflops=round(ff / ms_f / 1e9, 1),
              bwdq_ms=round(ms_q, 3), bwdkv_ms=round(ms_kv, 3),
              bwd_tflops=round(fb / (ms_q + ms_kv) / 1e9, 1),
              fwdbwd_tflops=round((ff + fb) / (ms_f + ms_q + ms_kv) / 1e9, 1),
