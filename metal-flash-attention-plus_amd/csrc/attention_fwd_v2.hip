@@ -298,19 +298,21 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Causal balance: 8 waves = two groups of 4.  A workgroup owns the mirrored pair of query
-// blocks (i, nblk-1-i) (equal causal work per workgroup); inside each block group 0 takes
-// the first half of the key tiles and group 1 the second half, and the two partial softmax
-// states (O, m, l) merge through LDS before group 0 stores the block.
-template <class E, int DP, int BK>
-__global__ void __launch_bounds__(512, 2) mfa_fwd2_pair_kernel(FwdParams p) {
-  constexpr int NT = 256, BQ = 128, ND = DP / 32;
+// Causal balance: two groups of NWG waves.  A workgroup owns the mirrored pair of query
+// blocks (i, nblk-1-i) of NWG*32 rows (equal causal work per workgroup); inside each block
+// group 0 takes the first half of the key tiles and group 1 the second half, and the two
+// partial softmax states (O, m, l) merge through LDS before group 0 stores the block.
+// NWG = 4: one 512-thread workgroup per CU; NWG = 2 (64-row blocks, BK = 32): two
+// independent 256-thread workgroups per CU, whose waves are not tied by a shared barrier.
+template <class E, int DP, int BK, int NWG>
+__global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p) {
+  constexpr int NT = NWG * 64, BQ = NWG * 32, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
-  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
-  const int gt = tid & 255;
+  const int g = __builtin_amdgcn_readfirstlane(tid / NT);
+  const int gt = tid % NT;
   const int lane = tid & 63, wg = gt >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
@@ -375,8 +377,8 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_pair_kernel(FwdParams p) {
     }
 
     // Merge group 1's partial state into group 0 through LDS (the staging ring is free).
-    float* mrg = reinterpret_cast<float*>(smem);        // [4 waves][ND*16][64]
-    float* mml = mrg + 4 * ND * 16 * 64;                // [4 waves][2][64]
+    float* mrg = reinterpret_cast<float*>(smem);        // [NWG waves][ND*16][64]
+    float* mml = mrg + NWG * ND * 16 * 64;              // [NWG waves][2][64]
     if (g == 1) {
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt)
@@ -420,11 +422,11 @@ static hipError_t launch_fwd2(const FwdParams& p, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <class E, int DP, int BK>
+template <class E, int DP, int BK, int NWG>
 static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 8 * BK * DP * 2;
-  static_assert(LDS >= 4 * (DP / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4, "merge area");
-  auto kern = mfa_fwd2_pair_kernel<E, DP, BK>;
+  static_assert(LDS >= NWG * (DP / 32) * 16 * 64 * 4 + NWG * 2 * 64 * 4, "merge area");
+  auto kern = mfa_fwd2_pair_kernel<E, DP, BK, NWG>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -432,8 +434,10 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int npairs = (p.nblk + 1) / 2;
-  hipLaunchKernelGGL(kern, dim3(npairs * p.B * p.H), dim3(512), LDS, stream, p);
+  FwdParams q = p;
+  q.nblk = (p.R + NWG * 32 - 1) / (NWG * 32);
+  const int npairs = (q.nblk + 1) / 2;
+  hipLaunchKernelGGL(kern, dim3(npairs * p.B * p.H), dim3(NWG * 128), LDS, stream, q);
   return hipGetLastError();
 }
 
@@ -457,10 +461,13 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
       }
     }
   }
-#define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                  \
-  if (elem == ELEM && DP == DPV)                                        \
-    return single ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)           \
-                  : launch_fwd2_pair<EE, DPV, BKV>(p, stream);
+  const char* pv = getenv("MFA_FWD_PAIR");
+  const bool pair64 = pv && pv[0] == '2';
+#define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                          \
+  if (elem == ELEM && DP == DPV)                                                \
+    return single ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)                   \
+                  : (pair64 ? launch_fwd2_pair<EE, DPV, 32, 2>(p, stream)       \
+                            : launch_fwd2_pair<EE, DPV, BKV, 4>(p, stream));
   MFA_F2(P_FP16, F16, 64, 64, 2)
   MFA_F2(P_FP16, F16, 128, 64, 2)
   MFA_F2(P_BF16, BF16, 64, 64, 2)
@@ -473,7 +480,8 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
 
 #define MFA_F2_INST(EE, DPV, BKV, WPS)                                        \
   template __global__ void mfa_fwd2_kernel<EE, DPV, BKV, WPS>(FwdParams);     \
-  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV>(FwdParams);
+  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV, 4>(FwdParams);  \
+  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, 32, 2>(FwdParams);
 MFA_F2_INST(F16, 64, 64, 2)
 MFA_F2_INST(F16, 128, 64, 2)
 MFA_F2_INST(BF16, 64, 64, 2)

@@ -62,16 +62,16 @@ def main():
                                             causal=True)
         desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
         for rnd in range(2):
-            for var, stg in (("pair", "0"), ("single", "0")):
+            for var, stg in (("pair", "4"), ("pair", "2"), ("single", "0")):
                 os.environ["MFA_FWD_VARIANT"] = var
-                os.environ["MFA_FWD_STAGGER"] = stg
+                os.environ["MFA_FWD_PAIR"] = stg
                 ms = time_it(lambda: mha.forward(desc, q, k, v, o, l, stream=stream),
                              args.reps * 5)
                 f = mfa.attention_flops(B, H, S, S, D, causal=True)
-                emit("C2", variant=var, stagger=stg, round=rnd, ms=round(ms, 4),
+                emit("C2", variant=var, pair_waves=stg, round=rnd, ms=round(ms, 4),
                      tflops=round(f / ms / 1e9, 1), frac=round(f / ms / 1e9 / PEAK, 4))
         os.environ.pop("MFA_FWD_VARIANT", None)
-        os.environ.pop("MFA_FWD_STAGGER", None)
+        os.environ.pop("MFA_FWD_PAIR", None)
         base_nc = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16)
         desc_nc = mfa.MultiHeadDescriptor.make(base_nc, B, H, S, D)
         ms = time_it(lambda: mha.forward(desc_nc, q, k, v, o, l, stream=stream), args.reps * 5)
