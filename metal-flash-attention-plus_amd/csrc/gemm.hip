@@ -13,6 +13,7 @@
 #include "../../include/mfa/mfa.h"
 #include "mfa_device.h"
 #include "mfa_params.h"
+#include "mfa_stage.h"
 #include "mfa_dispatch.h"
 
 namespace mfa {
@@ -153,7 +154,155 @@ __global__ void __launch_bounds__(256) mfa_gemm_kernel(GemmParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Tuned path for whole tiles: M % 128 == N % 128 == K % 64 == 0, 16-byte aligned rows, no
+// load-previous (the MLA decompression shape: [B·S, 512] x [512, H·D]).
+//   * computed transposed, D[n][m] = Σ_k B[k][n]·A[m][k]: the lane is m, the accumulator
+//     registers run along n, so the epilogue stores 4 consecutive n per register group (8-byte
+//     bf16 / 16-byte fp32 stores) instead of one element per store;
+//   * A [128 m][64 k] and B [64 k][128 n] tiles land by LDS-DMA in the TileA image, double
+//     buffered, one barrier per 64-deep k-step; B^T fragments by transposed reads, A fragments
+//     in the matching k order as two 8-byte reads.
+template <class E>
+__global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
+  constexpr int BM = 128, BN = 128, BK = 64;
+  using TAa = TileA<BK>;   // A tile: 128 rows of 64 k (128 B)
+  using TBb = TileA<BN>;   // B tile: 64 rows of 128 n (256 B)
+  using AB = Arith16<E, BN>;
+  constexpr int ATILE = BM * BK * 2, BTILE = BK * BN * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const ab = smem;
+  char* const bb = smem + 2 * ATILE;
+
+  const int z = blockIdx.z;
+  const char* A = (const char*)p.a + (p.b[1] ? 0 : z * p.sa * 2);
+  const char* B = (const char*)(p.b[1] ? p.b[z] : p.b[0]) + (p.b[1] ? 0 : z * p.sb * 2);
+  char* C = (char*)(p.b[1] ? p.c[z] : p.c[0]);
+  const int64_t coff = p.b[1] ? 0 : z * p.sc;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int trb[2] = {TBb::tr_base(lane, 0), TBb::tr_base(lane, 1)};
+  // A fragment in the k order of the transposed B read: element j of lane half h is
+  // k = 16s + 8(j>>2) + 4h + (j&3), i.e. bytes 8h..8h+7 of chunks 2s and 2s+1 of row m.
+  int abase[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) abase[c] = TAa::off(wm * 64 + l32, c) + 8 * hh;
+
+  DmaA<BK, BM, 256> ad;   // 128-byte rows
+  DmaA<BN, BK, 256> bd;   // 256-byte rows
+  ad.init(p.lda * 2, BM, BK * 2, tid);
+  bd.init(p.ldb * 2, BK, BN * 2, tid);
+  const char* ahead = A + (int64_t)m0 * p.lda * 2;
+  const char* bhead = B + (int64_t)n0 * 2;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+
+  ad.issue(ahead, 0, ab);
+  bd.issue(bhead, 0, bb);
+  wait_vm();
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < p.K; k0 += BK) {
+    if (k0 + BK < p.K) {
+      ad.issue(ahead + (int64_t)(k0 + BK) * 2, 0, ab + (cur ^ 1) * ATILE);
+      bd.issue(bhead + (int64_t)(k0 + BK) * p.ldb * 2, 0, bb + (cur ^ 1) * BTILE);
+    }
+    const char* at = ab + cur * ATILE;
+    const char* bt = bb + cur * BTILE;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      i16x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // rows wm*64 + 32i + l32: + 32 rows = 4 row blocks of TAa::RB; chunks 2s, 2s+1 live
+        // in column block s/2 (512 B) at chunk parities (2s)&3, (2s+1)&3.
+        const int cb = 512 * ((2 * s) >> 2);
+        const uint2 lo = *reinterpret_cast<const uint2*>(at + abase[(2 * s) & 3] + cb +
+                                                         TAa::RB * 4 * i);
+        const uint2 hi = *reinterpret_cast<const uint2*>(at + abase[(2 * s + 1) & 3] + cb +
+                                                         TAa::RB * 4 * i);
+        af[i] = __builtin_bit_cast(i16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bf[j] = AB::read_tr_a(bt, trb, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = E::mma(bf[j], af[i], acc[i][j]);
+    }
+    wait_vm();
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // acc[i][j][r] = C[m = m0 + wm*64 + 32i + l32][n = n0 + wn*64 + 32j + acc_row(r, hh)].
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + wm * 64 + i * 32 + l32;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 64 + j * 32 + 8 * g + 4 * hh;
+        const int64_t ci = coff + (int64_t)m * p.ldc + n;
+        const f32x16& a = acc[i][j];
+        if (p.prec_c == P_FP32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + ci) =
+              make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
+        } else {
+          const uint32_t w0 = (uint32_t)E::from_f32(a[4 * g]) | ((uint32_t)E::from_f32(a[4 * g + 1]) << 16);
+          const uint32_t w1 = (uint32_t)E::from_f32(a[4 * g + 2]) | ((uint32_t)E::from_f32(a[4 * g + 3]) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + ci) = make_uint2(w0, w1);
+        }
+      }
+  }
+}
+
+template <class E>
+static hipError_t launch_gemm2(const GemmParams& p, int batch, hipStream_t stream) {
+  constexpr int LDS = 2 * (128 * 64 * 2) + 2 * (64 * 128 * 2);
+  auto kern = mfa_gemm2_kernel<E>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const dim3 grid(p.N / 128, p.M / 128, batch);
+  hipLaunchKernelGGL(kern, grid, dim3(256), LDS, stream, p);
+  return hipGetLastError();
+}
+
+static bool gemm2_eligible(const GemmParams& p) {
+  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+    if (e[0] == '1') return false;
+  }
+  if (p.M % 128 || p.N % 128 || p.K % 64 || p.K == 0 || p.load_prev) return false;
+  if (p.lda % 8 || p.ldb % 8 || p.ldc % 8) return false;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (!al(p.a) || !al(p.b[0]) || !al(p.c[0])) return false;
+  if (p.b[1] && (!al(p.b[1]) || !al(p.c[1]))) return false;
+  if (!p.b[1] && (p.sa % 8 || p.sb % 8 || p.sc % 8)) return false;
+  // 32-bit buffer offsets per tile stream.
+  if ((int64_t)p.M * p.lda * 2 >= ((int64_t)1 << 31) || (int64_t)p.K * p.ldb * 2 >= ((int64_t)1 << 31))
+    return false;
+  return true;
+}
+
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream) {
+  if (gemm2_eligible(p)) {
+    if (prec_ab == P_FP16) return launch_gemm2<F16>(p, batch, stream);
+    if (prec_ab == P_BF16) return launch_gemm2<BF16>(p, batch, stream);
+  }
   const dim3 grid((p.N + 127) / 128, (p.M + 127) / 128, batch);
   if (prec_ab == P_FP16)
     hipLaunchKernelGGL(mfa_gemm_kernel<F16>, grid, dim3(256), 0, stream, p);
@@ -163,6 +312,9 @@ hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
+
+template __global__ void mfa_gemm2_kernel<F16>(GemmParams);
+template __global__ void mfa_gemm2_kernel<BF16>(GemmParams);
 
 }  // namespace mfa
 
