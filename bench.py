@@ -118,7 +118,7 @@ def main():
     # The variant the library picks for this shape (mfa_api.cpp launch_forward ->
     # attention_fwd_v2.hip fwd2_dispatch: causal with <= 768 row blocks runs the mirrored-pair
     # kernel, otherwise one 128-row block per workgroup).
-    kname = ("mfa_fwd2_pair_kernel<F16, 128, 64>" if (S + 127) // 128 * H * B <= 768
+    kname = ("mfa_fwd2_pair_kernel<F16, 128, 64, 4>" if (S + 127) // 128 * H * B <= 768
              else "mfa_fwd2_kernel<F16, 128, 64, 2>")
     result = {
         "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
