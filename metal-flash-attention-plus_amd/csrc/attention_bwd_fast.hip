@@ -227,13 +227,12 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     const bool diag = (p.mask.causal && t + BT - 1 > q0) || p.mask.window;
     if (diag) {
       MFA_KEEP_BRANCH();
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = t + j * 32 + acc_row(i, hh);
-          if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) s[j][i] = kMaskValue;
-        }
+      {
+        const int base = t + 4 * hh;
+        const int hi = p.mask.causal ? qi - base : 0x3fffffff;
+        const int lo = p.mask.window ? qi - wsz - base : -0x40000000;
+        mask_outside<NJ>(s, lo, hi, kMaskValue);
+      }
     }
     {
       constexpr int EPM = 16 / DS;  // P elements per dP MFMA (NJ*16 over DS*NJ MFMAs)
@@ -418,13 +417,13 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     auto apply_mask = [&]() {
       if ((p.mask.causal && k0 + BK - 1 > t) || p.mask.window) {
         MFA_KEEP_BRANCH();
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int q = t + j * 32 + acc_row(i, hh);
-            if ((p.mask.causal && ki > q) || (p.mask.window && q - ki > wsz)) s[j][i] = kMaskValue;
-          }
+        {
+          // Queries q = t + 4hh + kk stay for q >= ki (causal) and q <= ki + wsz (window).
+          const int base = t + 4 * hh;
+          const int lo = p.mask.causal ? ki - base : -0x40000000;
+          const int hi = p.mask.window ? ki + wsz - base : 0x3fffffff;
+          mask_outside<NJ>(s, lo, hi, kMaskValue);
+        }
       }
     };
     if constexpr (DP <= 128) {

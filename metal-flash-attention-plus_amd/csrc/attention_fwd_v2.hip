@@ -27,6 +27,22 @@
 
 namespace mfa {
 
+// Diagnostic build only (tools/diag/fwd_stamps.hip defines MFA_STAMPS): per-wave s_memrealtime
+// stamps (100 MHz) at phase boundaries, into a buffer no kernel output is computed from.
+#ifdef MFA_STAMPS
+__device__ unsigned long long g_mfa_stamps[1 << 20];
+#define MFA_STAMP(slot)                                                                     \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
+    if ((threadIdx.x & 63) == 0)                                                            \
+      g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (slot)] = t_; \
+  } while (0)
+#define MFA_STAMP_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define MFA_STAMP(slot) do {} while (0)
+#define MFA_STAMP_DRAIN() do {} while (0)
+#endif
+
 // Scheduling knobs (development A/B; the defaults are the shipped configuration): fragment
 // read-ahead for the QK^T and PV chains, MFMA-cluster priority, order pinning.
 template <int AHK_ = 4, int AHV_ = 3, bool PRIO_ = false, bool PIN_ = true>
@@ -90,14 +106,13 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
 
   if (mask_tile) {
     MFA_KEEP_BRANCH();
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = t + j * 32 + acc_row(i, hh);
-        if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz) || key >= p.C)
-          s[j][i] = -__builtin_inff();
-      }
+    // Keys t + 4hh + kk stay for lo <= kk <= hi: below C, at most qi (causal), at least
+    // qi - wsz (window).
+    const int base = t + 4 * hh;
+    int hi = p.C - 1 - base;
+    if (p.mask.causal) hi = min(hi, qi - base);
+    const int lo = p.mask.window ? qi - wsz - base : -0x40000000;
+    mask_outside<NJ>(s, lo, hi, -__builtin_inff());
   }
 
   float mx = s[0][0];
@@ -254,6 +269,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   }
   const int rb = p.nblk - 1 - blk;
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
+  MFA_STAMP(0);
   const int q0 = rb * BQ;
   const int qi = q0 + wave * 32 + l32;
   const bool qvalid = qi < p.R;
@@ -277,6 +293,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   st.init();
   wait_vm();
   __syncthreads();
+  MFA_STAMP(1);
 
   int cur = 0;
   for (int t = kbeg; t < kend; t += BK) {
@@ -292,9 +309,13 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
     cur ^= 1;
   }
 
+  MFA_STAMP(2);
   float l = cross_half_sum(st.lh) + kFltMin;
   if (!(l > 0.f)) l = kFltMin;
   if (qvalid) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+  MFA_STAMP(3);
+  MFA_STAMP_DRAIN();
+  MFA_STAMP(4);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -327,6 +348,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const float c = p.c_log2;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+  MFA_STAMP(0);
 
   DmaA<DP, BK, NT> kd, vd;
   kd.init((int)p.k.ss * 2, p.C, p.D * 2, gt);
@@ -358,6 +380,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
     st.init();
     wait_vm();
     __syncthreads();
+    MFA_STAMP(1 + 3 * which);
     int cur = 0;
     for (int step = 0; step < nA; ++step) {
       const int t = t0 + step * BK;
@@ -376,6 +399,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
       cur ^= 1;
     }
 
+    MFA_STAMP(2 + 3 * which);
     // Merge group 1's partial state into group 0 through LDS (the staging ring is free).
     float* mrg = reinterpret_cast<float*>(smem);        // [NWG waves][ND*16][64]
     float* mml = mrg + NWG * ND * 16 * 64;              // [NWG waves][2][64]
@@ -404,7 +428,10 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
       if (qvalid) store_o_l<DP>(p, st.o, mf, l, b, h, qi, hh);
     }
     __syncthreads();
+    MFA_STAMP(3 + 3 * which);
   }
+  MFA_STAMP_DRAIN();
+  MFA_STAMP(7);
 }
 
 template <class E, int DP, int BK, int WPS, class TU = TuneDefault>

@@ -289,6 +289,21 @@ __device__ __forceinline__ void xcd_unit_block(int bid, int units, int nblk, int
 // Row index (within a 32-row MFMA output tile) of accumulator register i in lane half h.
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+// Masks a tile of NJ 32x32 accumulators whose element (j, i) sits at offset
+// j*32 + acc_row(i, hh) along the accumulator row axis: elements whose offset (relative to
+// the lane's half-wave base, i.e. without the 4·hh term) lies outside [lo, hi] become `val`.
+// Compile-time offsets against two per-lane bounds: compares and selects, no branches.
+template <int NJ>
+__device__ __forceinline__ void mask_outside(f32x16 (&s)[NJ], int lo, int hi, float val) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = j * 32 + (i & 3) + 8 * (i >> 2);
+      s[j][i] = (kk < lo || kk > hi) ? val : s[j][i];
+    }
+}
+
 // Max / sum across the two 32-lane halves (lanes l and l^32 hold the same column).
 __device__ __forceinline__ float xhalf_max(float x) { return fmaxf(x, __shfl_xor(x, 32)); }
 __device__ __forceinline__ float xhalf_sum(float x) { return x + __shfl_xor(x, 32); }
