@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/mfa/mfa.h"
 #include "mfa_device.h"
 
@@ -124,6 +126,135 @@ __global__ void qz_quantize(const void* in, int prec, uint64_t n, uint32_t cols,
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Vector forms (the common case: 16-byte aligned input, 8 elements per thread step).  The
+// per-element arithmetic is the scalar kernels' (same division, rounding and clamping), so
+// the bytes are identical; the tensor-wise absmax reduces through LDS to one atomic per
+// workgroup (one atomic per wave on a single address serialised the reduction).
+template <int PREC>
+__device__ __forceinline__ void load8(const void* p, uint64_t v, float (&x)[8]) {
+  if constexpr (PREC == P_FP32) {
+    const float4 a = reinterpret_cast<const float4*>(p)[2 * v];
+    const float4 b = reinterpret_cast<const float4*>(p)[2 * v + 1];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[v];
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint16_t lo = (uint16_t)(w[k] & 0xffffu), hi = (uint16_t)(w[k] >> 16);
+      x[2 * k] = PREC == P_FP16 ? f16_to_f32(lo) : bf16_to_f32(lo);
+      x[2 * k + 1] = PREC == P_FP16 ? f16_to_f32(hi) : bf16_to_f32(hi);
+    }
+  }
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(256) qz_absmax_tensor_v(const void* in, uint64_t n,
+                                                          unsigned* ws) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const uint64_t n8 = n / 8, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  for (uint64_t v = gid; v < n8; v += stride) {
+    float x[8];
+    load8<PREC>(in, v, x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(x[k]));
+  }
+  for (uint64_t i = n8 * 8 + gid; i < n; i += stride) m = fmaxf(m, fabsf(load_any(in, PREC, i)));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(ws, abs_bits(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+// MODE 0 tensor-wise, 1 block-wise, 2 row-wise; requires cols % 8 == 0 (and bs % 8 == 0 for
+// block-wise) so that the 8 elements of a step share one scale.
+template <int PREC, int TARGET, int MODE>
+__global__ void __launch_bounds__(256) qz_quantize_v(const void* in, uint64_t n, uint32_t cols,
+                                                     uint32_t bs, uint32_t nbc,
+                                                     const float* scale_t, const float* scales,
+                                                     uint8_t* out) {
+  const uint64_t n8 = n / 8, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const float st = MODE == 0 ? scale_t[0] : 0.f;
+  for (uint64_t v = gid; v < n8; v += stride) {
+    float x[8];
+    load8<PREC>(in, v, x);
+    float s = st;
+    if constexpr (MODE != 0) {
+      const uint64_t i = v * 8, r = i / cols, c = i % cols;
+      s = scales[MODE == 1 ? (r / bs) * nbc + c / bs : r];
+    }
+    if constexpr (TARGET == P_INT8) {
+      uint32_t w[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        w[k >> 2] |= (uint32_t)(uint8_t)clamp8((int64_t)round_to_int(x[k] / s)) << (8 * (k & 3));
+      reinterpret_cast<uint2*>(out)[v] = make_uint2(w[0], w[1]);
+    } else {
+      uint32_t w = 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w |= nib((int64_t)round_to_int(x[k] / s) + 8) << (4 * k);
+      reinterpret_cast<uint32_t*>(out)[v] = w;
+    }
+  }
+  // Tail (n % 8 elements), element by element as in qz_quantize.
+  const uint64_t i0 = n8 * 8;
+  auto sc = [&](uint64_t i) -> float {
+    if constexpr (MODE == 0) return st;
+    const uint64_t r = i / cols, c = i % cols;
+    return scales[MODE == 1 ? (r / bs) * nbc + c / bs : r];
+  };
+  if constexpr (TARGET == P_INT8) {
+    for (uint64_t i = i0 + gid; i < n; i += stride)
+      reinterpret_cast<int8_t*>(out)[i] =
+          clamp8((int64_t)round_to_int(load_any(in, PREC, i) / sc(i)));
+  } else {
+    const uint64_t nbytes = (n + 1) / 2;
+    for (uint64_t t = i0 / 2 + gid; t < nbytes; t += stride) {
+      const uint64_t i = 2 * t;
+      const uint32_t lo = nib((int64_t)round_to_int(load_any(in, PREC, i) / sc(i)) + 8);
+      const uint32_t hi = i + 1 < n
+                              ? nib((int64_t)round_to_int(load_any(in, PREC, i + 1) / sc(i + 1)) + 8)
+                              : (MODE == 0 ? 8u : 0u);
+      out[t] = (uint8_t)((hi << 4) | lo);
+    }
+  }
+}
+
+// Row-wise absmax when a row is L = cols/8 vectors with L a power of two <= 64: 64/L rows per
+// wave, a row's vectors on L adjacent lanes, reduced by xor shuffles inside the lane group.
+template <int PREC>
+__global__ void __launch_bounds__(256) qz_absmax_rows_v(const void* in, uint32_t rows,
+                                                        uint32_t cols, float* scales,
+                                                        int32_t* zps, float div) {
+  const uint32_t L = cols / 8;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint32_t rpw = 64 / L;
+  for (uint64_t r0 = wave * rpw; r0 < rows; r0 += nwaves * rpw) {
+    const uint64_t r = r0 + lane / L;
+    float m = 0.f;
+    if (r < rows) {
+      float x[8];
+      load8<PREC>(in, r * L + lane % L, x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(x[k]));
+    }
+    for (uint32_t o = L / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, (int)o));
+    if (r < rows && lane % L == 0) {
+      scales[r] = m / div;
+      if (zps) zps[r] = 0;
+    }
+  }
+}
+
 __global__ void qz_dequantize(const uint8_t* in, int prec, uint64_t n, uint32_t cols, float scale,
                               int32_t zp, const float* bscale, const int32_t* bzp, uint32_t bs,
                               uint32_t nbc, float* out) {
@@ -147,6 +278,50 @@ thread_local char g_qerr[256];
 int grid_for(uint64_t n) {
   const uint64_t g = (n + 255) / 256;
   return (int)(g < 8192 ? (g == 0 ? 1 : g) : 8192);
+}
+// Grid of the vector kernels: one thread per 8 elements, at most 1024 workgroups (4 per CU).
+int grid_vec(uint64_t n) {
+  const uint64_t g = (n / 8 + 255) / 256;
+  return (int)(g < 1024 ? (g == 0 ? 1 : g) : 1024);
+}
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int PREC>
+void launch_absmax_v(const void* in, uint64_t n, unsigned* ws, hipStream_t s) {
+  hipLaunchKernelGGL(mfa::qz_absmax_tensor_v<PREC>, dim3(grid_vec(n)), dim3(256), 0, s, in, n, ws);
+}
+template <int PREC, int TARGET>
+void launch_quantize_v(int mode, const void* in, uint64_t n, uint32_t cols, uint32_t bs,
+                       uint32_t nbc, const float* st, const float* sc, uint8_t* out,
+                       hipStream_t s) {
+  const dim3 g(grid_vec(n)), b(256);
+  if (mode == 0)
+    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 0>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out);
+  else if (mode == 1)
+    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 1>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out);
+  else
+    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 2>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out);
+}
+template <int PREC>
+void launch_quantize_vp(int target, int mode, const void* in, uint64_t n, uint32_t cols,
+                        uint32_t bs, uint32_t nbc, const float* st, const float* sc, uint8_t* out,
+                        hipStream_t s) {
+  if (target == mfa::P_INT8)
+    launch_quantize_v<PREC, mfa::P_INT8>(mode, in, n, cols, bs, nbc, st, sc, out, s);
+  else
+    launch_quantize_v<PREC, mfa::P_INT4>(mode, in, n, cols, bs, nbc, st, sc, out, s);
+}
+// Vector quantise when the layout allows it; false: use the scalar kernel.
+bool quantize_vec(int prec, int target, int mode, const void* in, uint64_t n, uint32_t cols,
+                  uint32_t bs, uint32_t nbc, const float* st, const float* sc, uint8_t* out,
+                  hipStream_t s) {
+  if (!aligned16(in)) return false;
+  if (((uintptr_t)out & (target == mfa::P_INT8 ? 7 : 3)) != 0) return false;
+  if (mode != 0 && (cols % 8 != 0 || (mode == 1 && bs % 8 != 0))) return false;
+  if (prec == mfa::P_FP32) launch_quantize_vp<mfa::P_FP32>(target, mode, in, n, cols, bs, nbc, st, sc, out, s);
+  else if (prec == mfa::P_FP16) launch_quantize_vp<mfa::P_FP16>(target, mode, in, n, cols, bs, nbc, st, sc, out, s);
+  else launch_quantize_vp<mfa::P_BF16>(target, mode, in, n, cols, bs, nbc, st, sc, out, s);
+  return true;
 }
 }  // namespace
 
@@ -175,13 +350,24 @@ extern "C" mfa_status_t mfa_quantize(const void* input, int32_t input_precision,
   if (mode == MFA_QUANT_TENSOR_WISE) {
     if (!workspace || !scale_out) return MFA_ERR_INVALID_ARGUMENT;
     if (hipMemsetAsync(workspace, 0, 16, s) != hipSuccess) return MFA_ERR_LAUNCH;
-    hipLaunchKernelGGL(qz_absmax_tensor, dim3(grid_for(count)), dim3(256), 0, s, input,
-                       input_precision, count, (unsigned*)workspace);
+    if (aligned16(input)) {
+      if (input_precision == MFA_PRECISION_FP32)
+        launch_absmax_v<P_FP32>(input, count, (unsigned*)workspace, s);
+      else if (input_precision == MFA_PRECISION_FP16)
+        launch_absmax_v<P_FP16>(input, count, (unsigned*)workspace, s);
+      else
+        launch_absmax_v<P_BF16>(input, count, (unsigned*)workspace, s);
+    } else {
+      hipLaunchKernelGGL(qz_absmax_tensor, dim3(grid_for(count)), dim3(256), 0, s, input,
+                         input_precision, count, (unsigned*)workspace);
+    }
     hipLaunchKernelGGL(qz_scale_tensor, dim3(1), dim3(64), 0, s, (const unsigned*)workspace,
                        scale_out, div);
-    hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
-                       input_precision, count, cols ? cols : 1u, target_precision, 0, 1u, 1u,
-                       (const float*)scale_out, (const float*)nullptr, (uint8_t*)output);
+    if (!quantize_vec(input_precision, target_precision, 0, input, count, cols ? cols : 1u, 1u,
+                      1u, scale_out, nullptr, (uint8_t*)output, s))
+      hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
+                         input_precision, count, cols ? cols : 1u, target_precision, 0, 1u, 1u,
+                         (const float*)scale_out, (const float*)nullptr, (uint8_t*)output);
   } else if (mode == MFA_QUANT_BLOCKWISE || mode == MFA_QUANT_ROW_WISE) {
     if (!block_scales_out || rows == 0 || cols == 0) return MFA_ERR_INVALID_ARGUMENT;
     uint32_t bsr, bsc, nbr, nbc;
@@ -193,13 +379,33 @@ extern "C" mfa_status_t mfa_quantize(const void* input, int32_t input_precision,
     } else {
       bsr = 1; bsc = cols; nbr = rows; nbc = 1;
     }
-    hipLaunchKernelGGL(qz_absmax_groups, dim3(nbr * nbc), dim3(256), 0, s, input, input_precision,
-                       count, rows, cols, bsr, bsc, nbc, block_scales_out, block_zero_points_out,
-                       div);
-    hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
-                       input_precision, count, cols, target_precision,
-                       mode == MFA_QUANT_BLOCKWISE ? 1 : 2, block_size ? block_size : 1u, nbc,
-                       (const float*)nullptr, (const float*)block_scales_out, (uint8_t*)output);
+    const uint32_t L = cols / 8;
+    const bool rows_v = mode == MFA_QUANT_ROW_WISE && cols % 8 == 0 && L <= 64 &&
+                        (L & (L - 1)) == 0 && aligned16(input) && (uint64_t)rows * cols == count;
+    if (rows_v) {
+      const uint64_t waves = ((uint64_t)rows * L + 63) / 64;
+      const int grid = (int)std::min<uint64_t>((waves + 3) / 4, 4096);
+      if (input_precision == MFA_PRECISION_FP32)
+        hipLaunchKernelGGL(qz_absmax_rows_v<P_FP32>, dim3(grid), dim3(256), 0, s, input, rows, cols,
+                           block_scales_out, block_zero_points_out, div);
+      else if (input_precision == MFA_PRECISION_FP16)
+        hipLaunchKernelGGL(qz_absmax_rows_v<P_FP16>, dim3(grid), dim3(256), 0, s, input, rows, cols,
+                           block_scales_out, block_zero_points_out, div);
+      else
+        hipLaunchKernelGGL(qz_absmax_rows_v<P_BF16>, dim3(grid), dim3(256), 0, s, input, rows, cols,
+                           block_scales_out, block_zero_points_out, div);
+    } else {
+      hipLaunchKernelGGL(qz_absmax_groups, dim3(nbr * nbc), dim3(256), 0, s, input,
+                         input_precision, count, rows, cols, bsr, bsc, nbc, block_scales_out,
+                         block_zero_points_out, div);
+    }
+    const int qmode = mode == MFA_QUANT_BLOCKWISE ? 1 : 2;
+    const uint32_t bsz = block_size ? block_size : 1u;
+    if (!quantize_vec(input_precision, target_precision, qmode, input, count, cols, bsz, nbc,
+                      nullptr, block_scales_out, (uint8_t*)output, s))
+      hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
+                         input_precision, count, cols, target_precision, qmode, bsz, nbc,
+                         (const float*)nullptr, (const float*)block_scales_out, (uint8_t*)output);
   } else {
     return MFA_ERR_INVALID_DESCRIPTOR;
   }

@@ -61,6 +61,46 @@ def test_runtime_quantize_rowwise_scales(gpu):
 
 
 @pytest.mark.parametrize("target", [P.INT8, P.INT4])
+@pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
+def test_runtime_quantize_large_vector_paths(gpu, target, src):
+    # 2049 x 1024 elements: the 8-wide kernels with several grid-stride steps per thread, and
+    # a misaligned view (offset by one element) through the scalar kernels.
+    rows, cols = 2049, 1024
+    x = (np.random.default_rng(5).standard_normal((rows, cols)) * 2).astype(np.float32)
+    xt = tdev(x, src)
+    xs = xt.float().cpu().numpy()
+    data, scale, _, _ = mfa.quantize(xt, target, rows=rows, cols=cols)
+    torch.cuda.synchronize()
+    s_ref = ol.quant_scale_tensor(xs, int(target))
+    assert scale.item() == np.float32(s_ref)
+    assert np.array_equal(data.cpu().numpy(), ol.quantize(xs, int(target), s_ref))
+    flat = xt.reshape(-1)[1:]
+    data1, scale1, _, _ = mfa.quantize(flat, target, rows=1, cols=flat.numel())
+    torch.cuda.synchronize()
+    s1 = ol.quant_scale_tensor(xs.reshape(-1)[1:], int(target))
+    assert scale1.item() == np.float32(s1)
+    assert np.array_equal(data1.cpu().numpy(), ol.quantize(xs.reshape(-1)[1:], int(target), s1))
+    # Row-wise and block-wise on the same data (cols % 8 == 0: vector kernels).
+    _, _, rsc, _ = mfa.quantize(xt, target, mfa.QuantMode.rowWise, rows, cols)
+    dat_b, _, bsc, _ = mfa.quantize(xt, target, mfa.QuantMode.blockwise, rows, cols, 64)
+    torch.cuda.synchronize()
+    assert np.array_equal(rsc.cpu().numpy(), ol.quant_scales_row(xs, rows, cols, int(target)))
+    b_ref = ol.quant_scales_block(xs, rows, cols, 64, int(target))
+    assert np.array_equal(bsc.cpu().numpy(), b_ref)
+    assert np.array_equal(dat_b.cpu().numpy(), ol.quantize_block(xs, cols, 64, int(target), b_ref))
+    # Row-wise with 128-element rows (C3's head dim): 4 rows per wave.
+    x128 = xt.reshape(-1, 128)
+    dat_r, _, rsc2, _ = mfa.quantize(x128, target, mfa.QuantMode.rowWise, x128.shape[0], 128)
+    torch.cuda.synchronize()
+    r_ref = ol.quant_scales_row(xs.reshape(-1, 128), x128.shape[0], 128, int(target))
+    assert np.array_equal(rsc2.cpu().numpy(), r_ref)
+    if target == P.INT8:
+        q = dat_r.cpu().numpy().view(np.int8).reshape(-1, 128)
+        for r in (0, 1, 777, x128.shape[0] - 1):
+            assert np.array_equal(q[r], ol.quantize(xs.reshape(-1, 128)[r], int(target), r_ref[r]).view(np.int8))
+
+
+@pytest.mark.parametrize("target", [P.INT8, P.INT4])
 def test_dequantize_bitexact(gpu, target):
     x = np.random.default_rng(11).standard_normal(1001).astype(np.float32)
     s = ol.quant_scale_tensor(x, int(target))

@@ -1,6 +1,6 @@
 // fwd_stamps.hip — diagnostic build of the v2 forward with per-wave phase stamps
 // (development tool; not part of libmfa_amd.so).  Build: make -C tools/diag
-// Run: tools/diag/fwd_stamps [H] [S] [causal] [variant s|p] [reps]
+// Run: tools/diag/fwd_stamps [H] [S] [causal] [variants, e.g. s,p,3] [reps] [D]
 // Prints, per stamp slot, the spread over waves of (slot time − kernel's first start), µs.
 #define MFA_STAMPS 1
 #include "../../metal-flash-attention-plus_amd/csrc/attention_fwd_v2.hip"
@@ -38,7 +38,8 @@ int main(int argc, char** argv) {
   const int causal = argc > 3 ? atoi(argv[3]) : 1;
   const char* var = argc > 4 ? argv[4] : "p";
   const int reps = argc > 5 ? atoi(argv[5]) : 400;
-  const int B = 1, D = 128;
+  const int B = 1;
+  const int D = argc > 6 ? atoi(argv[6]) : 128;
   const size_t n = (size_t)B * H * S * D;
   uint16_t *q, *k, *v, *l;
   float* o;
@@ -88,7 +89,7 @@ int main(int argc, char** argv) {
   double fl = 4.0 * D * (causal ? (double)S * (S + 1) / 2 : (double)S * S) * B * H;
   for (int i = 0; i < reps; ++i) {
     set_var(vars[i % vars.size()]);
-    CK(mfa::fwd2_dispatch(p, mfa::P_FP16, 128, st));
+    CK(mfa::fwd2_dispatch(p, mfa::P_FP16, D, st));
   }
   const int timed = 50;
   std::vector<std::vector<float>> res(vars.size());
@@ -96,7 +97,7 @@ int main(int argc, char** argv) {
     for (size_t vi = 0; vi < vars.size(); ++vi) {
       set_var(vars[vi]);
       CK(hipEventRecord(e0, st));
-      for (int i = 0; i < timed; ++i) CK(mfa::fwd2_dispatch(p, mfa::P_FP16, 128, st));
+      for (int i = 0; i < timed; ++i) CK(mfa::fwd2_dispatch(p, mfa::P_FP16, D, st));
       CK(hipEventRecord(e1, st));
       CK(hipStreamSynchronize(st));
       float ms;
@@ -115,7 +116,7 @@ int main(int argc, char** argv) {
   void* dsym;
   CK(hipGetSymbolAddress(&dsym, HIP_SYMBOL(mfa::g_mfa_stamps)));
   CK(hipMemset(dsym, 0, sizeof(unsigned long long) << 20));
-  CK(mfa::fwd2_dispatch(p, mfa::P_FP16, 128, st));
+  CK(mfa::fwd2_dispatch(p, mfa::P_FP16, D, st));
   CK(hipStreamSynchronize(st));
   CK(hipMemcpy(stamps.data(), dsym, sizeof(unsigned long long) << 20, hipMemcpyDeviceToHost));
   unsigned long long t0 = ~0ull, tend = 0;
