@@ -28,6 +28,45 @@
 
 namespace mfa {
 
+// D = 256 backwardKeyValue schedule: softmax work threaded between the MFMAs (true) or the
+// dual-chain schedule with the softmax as one block (false).
+constexpr bool kBwdKv256Interleave = true;
+// backwardKeyValue: stage the next Q/dO tiles piece by piece between the first chain's MFMAs
+// (D = 256: 5.03 vs 5.18 ms at B4 H32 S4096) or all at once at the top of the step (D <= 128:
+// 2.78 vs 3.30 ms; tools/diag/bwd_stamps).
+#ifndef MFA_SPREAD_MIN_DP
+#define MFA_SPREAD_MIN_DP 256
+#endif
+template <int DP>
+constexpr bool spread_dma() { return DP >= MFA_SPREAD_MIN_DP; }
+
+// Diagnostic build only (tools/diag/bwd_stamps.hip defines MFA_BSTAMPS): per-wave shader-clock
+// totals of the backwardKeyValue phases, into a buffer no output is computed from.
+#ifdef MFA_BSTAMPS
+__device__ unsigned long long g_mfa_bstamps[1 << 18];
+#define BST_DECL()                               \
+  unsigned long long bst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long bst_t = __builtin_amdgcn_s_memtime()
+#define BST(slot)                                               \
+  do {                                                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    bst_acc[slot] += t_ - bst_t;                                \
+    bst_t = t_;                                                 \
+  } while (0)
+#define BST_END()                                                                  \
+  do {                                                                             \
+    if ((threadIdx.x & 63) == 0)                                                   \
+      for (int s_ = 0; s_ < 8; ++s_)                                               \
+        g_mfa_bstamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + s_] = \
+            bst_acc[s_];                                                           \
+  } while (0)
+#else
+#define BST_DECL() do {} while (0)
+#define BST(slot) do {} while (0)
+#define BST_END() do {} while (0)
+#endif
+
+
 // Row fragments of one row (16-bit, contiguous): elements d = 16*s + 8*hh + j.
 template <int DP>
 __device__ __forceinline__ void load_frags16(i16x8 (&f)[DP / 16], const uint16_t* row, bool valid,
@@ -43,11 +82,11 @@ __device__ __forceinline__ void load_frags16(i16x8 (&f)[DP / 16], const uint16_t
 // Two MFMA chains over the head dimension sharing the register operand index:
 //   acc1[j] += A1(rows j*32..) · b1[ds],  acc2[j] += A2(rows j*32..) · b2[ds]
 // with A fragments read from LDS row tiles AH instructions ahead of their MFMA.
-template <class A, int NJ>
+template <class A, int NJ, class Hook>
 __device__ __forceinline__ void dual_rows_chain(const char* t1, const char* t2,
                                                 const i16x8* b1, const i16x8* b2,
                                                 f32x16 (&acc1)[NJ], f32x16 (&acc2)[NJ],
-                                                const int (&rbase)[2]) {
+                                                const int (&rbase)[2], Hook&& hook) {
   constexpr int NM = A::DSTEPS * NJ * 2;
   constexpr int AH = 4;
   i16x8 fr[AH];
@@ -67,6 +106,7 @@ __device__ __forceinline__ void dual_rows_chain(const char* t1, const char* t2,
     else
       acc1[j] = A::mma(fr[i % AH], b1[ds], acc1[j]);
     if (i + AH < NM) fr[i % AH] = rd(i + AH);
+    hook(i);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -74,18 +114,18 @@ __device__ __forceinline__ void dual_rows_chain(const char* t1, const char* t2,
 // acc[j] += A(rows j*32.. of an LDS row tile, k-step ds) · b[ds] over all (ds, j), fragment
 // reads AH MFMAs ahead, order pinned; after MFMA i the hook runs VALU slice i, so work that
 // does not feed this chain (the previous product's softmax) issues between its MFMAs.
-template <class A, int NJ, class Hook>
+template <class A, int NJ, bool ZERO = false, class Hook>
 __device__ __forceinline__ void rows_chain(const char* tile, const i16x8* b, f32x16 (&acc)[NJ],
                                            const int (&rbase)[2], Hook&& hook) {
   constexpr int NM = A::DSTEPS * NJ;
-  constexpr int AH = A::DSTEPS >= 16 ? 2 : 4;  // D=256 runs at the 512-register limit
+  constexpr int AH = A::DSTEPS >= 16 ? 3 : 4;  // D=256 runs at the 512-register limit
   i16x8 fr[AH];
 #pragma unroll
   for (int i = 0; i < AH; ++i) fr[i] = A::read_row_a(tile, rbase, i % NJ, i / NJ);
 #pragma unroll
   for (int i = 0; i < NM; ++i) {
     const int ds = i / NJ, j = i % NJ;
-    acc[j] = A::mma(fr[i % AH], b[ds], acc[j]);
+    acc[j] = A::mma(fr[i % AH], b[ds], (ZERO && ds == 0) ? zero16() : acc[j]);
     if (i + AH < NM) fr[i % AH] = A::read_row_a(tile, rbase, (i + AH) % NJ, (i + AH) / NJ);
     hook(i);
     __builtin_amdgcn_sched_barrier(0);
@@ -98,7 +138,7 @@ template <class A, int NJ, int ND, class Hook>
 __device__ __forceinline__ void tr_chain(const char* tile, const int (&trb)[2], const i16x8* b,
                                          f32x16 (&acc)[ND], Hook&& hook) {
   constexpr int NM = NJ * 2 * ND;
-  constexpr int AH = ND >= 8 ? 2 : 3;
+  constexpr int AH = 3;
   i16x8 fr[AH];
 #pragma unroll
   for (int i = 0; i < AH; ++i) {
@@ -346,28 +386,31 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   };
   // L and D of the step's BQ query rows: one value per thread of the first BQ threads, staged
   // through registers into LDS (converted to fp32); L = +inf past R makes P = dS = 0 there.
-  float lreg = 0.f, dreg = 0.f;
+  // The loads leave raw bits in registers and are converted only at the step's end, so their
+  // latency hides under the step (a conversion right after the load waits for it).
+  uint32_t lraw = 0u, draw = 0u;
+  bool ldv = false;
   auto ld_load = [&](int h, int t) {
     if (tid < BQ) {
       const int q = t + tid;
-      const int64_t r = (int64_t)(b * p.H + h) * p.R + q;
-      lreg = __builtin_inff();
-      dreg = 0.f;
-      if (q < p.R) {
-        lreg = p.l_f16 ? f16_to_f32(reinterpret_cast<const uint16_t*>(p.l)[r])
-                       : reinterpret_cast<const float*>(p.l)[r];
-        dreg = p.d_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p.dD)[r])
-                        : reinterpret_cast<const float*>(p.dD)[r];
-      }
+      ldv = q < p.R;
+      const int64_t r = (int64_t)(b * p.H + h) * p.R + (ldv ? q : 0);
+      lraw = p.l_f16 ? (uint32_t)reinterpret_cast<const uint16_t*>(p.l)[r]
+                     : reinterpret_cast<const uint32_t*>(p.l)[r];
+      draw = p.d_bf16 ? (uint32_t)reinterpret_cast<const uint16_t*>(p.dD)[r]
+                      : reinterpret_cast<const uint32_t*>(p.dD)[r];
     }
   };
   auto ld_store = [&](int buf) {
     if (tid < BQ) {
-      lb0[buf * BQ + tid] = lreg;
-      db0[buf * BQ + tid] = dreg;
+      const float lv = p.l_f16 ? f16_to_f32((uint16_t)lraw) : __builtin_bit_cast(float, lraw);
+      const float dv = p.d_bf16 ? bf16_to_f32((uint16_t)draw) : __builtin_bit_cast(float, draw);
+      lb0[buf * BQ + tid] = ldv ? lv : __builtin_inff();
+      db0[buf * BQ + tid] = ldv ? dv : 0.f;
     }
   };
 
+  BST_DECL();
   f32x16 dk[ND], dv[ND];
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
@@ -381,21 +424,39 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     wait_vm();
     ld_store(0);
   }
+  // Unconditionally drained before the loop: otherwise the K/V fragment loads count as
+  // possibly pending at the loop header and hipcc puts a vmcnt(0) before their first use in
+  // every step (which then also waits for the step's own prefetch).
+  wait_vm();
   __syncthreads();
+  BST(7);
 
   int cur = 0;
   for (int step = 0; step < nsteps; ++step) {
     const int g = step / ntile;
     const int t = qbeg + (step - g * ntile) * BQ;
     const bool has_next = step + 1 < nsteps;
-    if (has_next) {
-      const int gn = (step + 1) / ntile;
-      const int tn = qbeg + (step + 1 - gn * ntile) * BQ;
-      const int hn = kvh + gn * p.Hkv;
+    const int gn = (step + 1) / ntile;
+    const int tn = qbeg + (step + 1 - gn * ntile) * BQ;
+    const int hn = kvh + gn * p.Hkv;
+    if (has_next) ld_load(hn, tn);
+    if (!spread_dma<DP>() && has_next) {
       qd.issue(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB);
       od.issue(ohead(hn), tn, ob0 + (cur ^ 1) * TILEB);
-      ld_load(hn, tn);
     }
+    BST(0);
+    // The next step's Q and dO tiles: one LDS-DMA piece after every other MFMA of the first
+    // chain, so each piece's issue cost sits in an MFMA gap.
+    auto dma_hook = [&](int i) {
+      constexpr int PPW = DmaA<DP, BQ, NT>::PPW;
+      if (spread_dma<DP>() && (i & 1) == 0 && i / 2 < 2 * PPW && has_next) {
+        const int k = i / 2;
+        if (k < PPW)
+          qd.issue_piece(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB, k);
+        else
+          od.issue_piece(ohead(hn), tn, ob0 + (cur ^ 1) * TILEB, k - PPW);
+      }
+    };
     const char* qt = qb0 + cur * TILEB;
     const char* ot = ob0 + cur * TILEB;
     const float* lt = lb0 + cur * BQ;
@@ -429,43 +490,104 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     if constexpr (DP <= 128) {
       // S = Q·K^T; masks; dP = dO·V^T with P = exp2(S·c − L) computed between its MFMAs;
       // dV^T += dO^T·P with dS = P∘(dP·scale − D) computed between its MFMAs; dK^T += Q^T·dS.
-      rows_chain<A, NJ>(qt, kf, s, rbase, [](int) {});
+      // The S and dP accumulators are read once each into VGPR values (P, and dS eight at a
+      // time), never updated in place: in-place updates of MFMA accumulators cost a
+      // register-file copy per element each way.
+      auto pack8 = [](const float* x) {
+        i16x8 f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (short)E::from_f32(x[e]);
+        return f;
+      };
+      rows_chain<A, NJ, true>(qt, kf, s, rbase, dma_hook);
       apply_mask();
+      BST(1);
+      float pf[NJ][16];
       {
         float lv[NJ][16];
         lds4(lt, lv);
         constexpr int EPM = 16 / DS;
-        rows_chain<A, NJ>(ot, vf, dp, rbase, [&](int i) {
+        rows_chain<A, NJ, true>(ot, vf, dp, rbase, [&](int i) {
 #pragma unroll
           for (int e = 0; e < EPM; ++e) {
             const int idx = i * EPM + e, jj = idx >> 4, ii = idx & 15;
-            s[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -lv[jj][ii]));
+            pf[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -lv[jj][ii]));
           }
         });
       }
+      BST(2);
       i16x8 pb[NJ * 2], sb[NJ * 2];
 #pragma unroll
-      for (int jk = 0; jk < NJ * 2; ++jk) pb[jk] = A::pack(s[jk >> 1], jk & 1);
+      for (int jk = 0; jk < NJ * 2; ++jk) pb[jk] = pack8(&pf[jk >> 1][8 * (jk & 1)]);
       float dv_[NJ][16];
       lds4(dtl, dv_);
       constexpr int NMV = NJ * 2 * ND;
       constexpr int EPM = (NJ * 16 + NMV - 1) / NMV;
+      float d8[8];
       tr_chain<A, NJ, ND>(ot, trb, pb, dv, [&](int i) {
 #pragma unroll
         for (int e = 0; e < EPM; ++e) {
           const int idx = i * EPM + e;
           if (idx < NJ * 16) {
             const int jj = idx >> 4, ii = idx & 15;
-            dp[jj][ii] = s[jj][ii] * __builtin_fmaf(dp[jj][ii], sc, -dv_[jj][ii]);
-            if ((ii & 7) == 7) sb[jj * 2 + (ii >> 3)] = A::pack(dp[jj], ii >> 3);
+            d8[ii & 7] = pf[jj][ii] * __builtin_fmaf(dp[jj][ii], sc, -dv_[jj][ii]);
+            if ((ii & 7) == 7) sb[jj * 2 + (ii >> 3)] = pack8(d8);
           }
         }
       });
+      BST(3);
+      tr_chain<A, NJ, ND>(qt, trb, sb, dk, [](int) {});
+      BST(4);
+    } else if constexpr (kBwdKv256Interleave) {
+      // D = 256 at the 512-register limit: the interleave above, with L and D read from LDS
+      // four rows at a time inside the hooks (one group ahead) instead of held for the tile.
+      auto ldg = [&](const float* base, int grp, float (&v)[4]) {
+        const float4 x =
+            *reinterpret_cast<const float4*>(base + (grp >> 2) * 32 + 8 * (grp & 3) + 4 * hh);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      };
+      constexpr int NG = NJ * 4;  // 4-row groups of the tile
+      // S and dP chains together (the registers do not hold a hook's working set beside
+      // both chains), then P, then dS threaded through the dV chain.
+      dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase, dma_hook);
+      apply_mask();
+#pragma unroll
+      for (int grp = 0; grp < NG; ++grp) {
+        float lq[4];
+        ldg(lt, grp, lq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int idx = grp * 4 + k, jj = idx >> 4, ii = idx & 15;
+          s[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -lq[k]));
+        }
+      }
+      i16x8 pb[NJ * 2], sb[NJ * 2];
+#pragma unroll
+      for (int jk = 0; jk < NJ * 2; ++jk) pb[jk] = A::pack(s[jk >> 1], jk & 1);
+      {
+        constexpr int NMV = NJ * 2 * ND;
+        constexpr int EPM = (NJ * 16 + NMV - 1) / NMV;
+        float dq[2][4];
+        ldg(dtl, 0, dq[0]);
+        tr_chain<A, NJ, ND>(ot, trb, pb, dv, [&](int i) {
+#pragma unroll
+          for (int e = 0; e < EPM; ++e) {
+            const int idx = i * EPM + e;
+            if (idx < NJ * 16) {
+              const int jj = idx >> 4, ii = idx & 15;
+              const int grp = idx >> 2, k = idx & 3;
+              if (k == 0 && grp + 1 < NG) ldg(dtl, grp + 1, dq[(grp + 1) & 1]);
+              dp[jj][ii] = s[jj][ii] * __builtin_fmaf(dp[jj][ii], sc, -dq[grp & 1][k]);
+              if ((ii & 7) == 7) sb[jj * 2 + (ii >> 3)] = A::pack(dp[jj], ii >> 3);
+            }
+          }
+        });
+      }
       tr_chain<A, NJ, ND>(qt, trb, sb, dk, [](int) {});
     } else {
-      // D = 256 runs at the register limit: S and dP chains together, then the softmax, then
+      // D = 256 (previous schedule) runs at the register limit: S and dP chains together, then the softmax, then
       // dV and dK together.
-      dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase);
+      dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase, dma_hook);
       apply_mask();
       float lv[NJ][16], dv_[NJ][16];
       lds4(lt, lv);
@@ -509,10 +631,13 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       }
     }
     wait_vm();
+    BST(5);
     if (has_next) ld_store(cur ^ 1);
     __syncthreads();
+    BST(6);
     cur ^= 1;
   }
+  BST_END();
 
   if (kvalid) {
     const int64_t krow = (int64_t)(b * p.Hkv + kvh) * p.C + ki;

@@ -391,14 +391,30 @@ struct DmaA {
   }
   __device__ __forceinline__ void issue(const char* head, int t, char* dst) const {
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int n = w + NW * i;
-      const int rb = t * step;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(head + rb), (short)0, max(bytes - rb, 0), 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(dst + n * 1024), 16, off[i], 0, 0, 0);
-    }
+    for (int i = 0; i < PPW; ++i) issue_piece(head, t, dst, i);
+  }
+  // Piece i (< PPW) of this wave's share alone: spread over the MFMAs of a chain, each
+  // piece's issue cost hides in an MFMA gap instead of queueing behind the others.
+  // Issued as inline asm: the compiler then knows nothing of the LDS write, so it does not
+  // guard every later ds_read with vmcnt(0) (it cannot tell the slot being filled from the
+  // slot being read); the caller's wait_vm() + barrier order the tile instead.
+  __device__ __forceinline__ void issue_piece(const char* head, int t, char* dst, int i) const {
+    const int n = w + NW * i;
+    const int rb = t * step;
+    const uint64_t base = (uint64_t)(uintptr_t)(head + rb);
+    const int nrec = max(bytes - rb, 0);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 rs;
+    rs[0] = __builtin_amdgcn_readfirstlane((unsigned)base);
+    rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32) & 0xffffu);
+    rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
+    rs[3] = 0x00020000u;
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(dst + n * 1024)));
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                 :
+                 : "v"(off[i]), "s"(rs), "s"(lds)
+                 : "memory", "m0");
   }
 };
 

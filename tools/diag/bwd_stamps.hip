@@ -1,0 +1,99 @@
+// bwd_stamps.hip — diagnostic build of the fast backward with per-wave phase cycle totals of
+// backwardKeyValue (development tool; not part of libmfa_amd.so).  Build: make -C tools/diag
+// Run: tools/diag/bwd_stamps [B] [H] [S] [D]   (fp16, non-causal)
+#define MFA_BSTAMPS 1
+#include "../../metal-flash-attention-plus_amd/csrc/attention_bwd_fast.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+__global__ void fill_rand16(uint16_t* x, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    x[i] = mfa::F16::from_f32(((h & 0xffff) / 65535.f * 2.f - 1.f) * 0.25f);
+  }
+}
+__global__ void fill_const32(float* x, size_t n, float v) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) x[i] = v;
+}
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 4;
+  const int H = argc > 2 ? atoi(argv[2]) : 32;
+  const int S = argc > 3 ? atoi(argv[3]) : 4096;
+  const int D = argc > 4 ? atoi(argv[4]) : 128;
+  const size_t n = (size_t)B * H * S * D;
+  uint16_t *q, *k, *v, *dO;
+  float *l, *dd, *o, *dq, *dk, *dv;
+  CK(hipMalloc(&q, n * 2)); CK(hipMalloc(&k, n * 2)); CK(hipMalloc(&v, n * 2)); CK(hipMalloc(&dO, n * 2));
+  CK(hipMalloc(&o, n * 4)); CK(hipMalloc(&dq, n * 4)); CK(hipMalloc(&dk, n * 4)); CK(hipMalloc(&dv, n * 4));
+  CK(hipMalloc(&l, (size_t)B * H * S * 4)); CK(hipMalloc(&dd, (size_t)B * H * S * 4));
+  fill_rand16<<<1024, 256>>>(q, n, 1); fill_rand16<<<1024, 256>>>(k, n, 2);
+  fill_rand16<<<1024, 256>>>(v, n, 3); fill_rand16<<<1024, 256>>>(dO, n, 4);
+  fill_const32<<<1024, 256>>>(l, (size_t)B * H * S, 12.f);
+  fill_const32<<<1024, 256>>>(dd, (size_t)B * H * S, 0.01f);
+  mfa::BwdParams p;
+  memset(&p, 0, sizeof(p));
+  auto op = [&](const void* ptr) {
+    mfa::Operand x;
+    memset(&x, 0, sizeof(x));
+    x.ptr = ptr; x.ss = D; x.sh = (int64_t)S * D; x.sb = (int64_t)H * S * D; x.sd = 1;
+    x.prec = mfa::P_FP16; x.vec = 1; x.scale = 1.f; x.cols = D;
+    return x;
+  };
+  p.q = op(q); p.k = op(k); p.v = op(v); p.dO_op = op(dO);
+  p.o = o; p.l = l; p.l_f16 = 0; p.dD = dd; p.d_bf16 = 0;
+  p.dq = dq; p.dk = dk; p.dv = dv;
+  p.B = B; p.H = H; p.Hkv = H; p.R = S; p.C = S; p.D = D; p.group = 1;
+  const float scale = 1.f / sqrtf((float)D);
+  p.c_log2 = 1.442695041f * scale; p.scale = scale; p.dscale = scale; p.dq_mul = 1.f; p.dk_mul = 1.f;
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int i = 0; i < 5; ++i) CK(mfa::bwd_fast_dispatch(p, 1, mfa::P_FP16, D, st));
+  CK(hipEventRecord(e0, st));
+  for (int i = 0; i < 5; ++i) CK(mfa::bwd_fast_dispatch(p, 1, mfa::P_FP16, D, st));
+  CK(hipEventRecord(e1, st));
+  CK(hipStreamSynchronize(st));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= 5;
+  const double fl = 8.0 * D * (double)S * S * B * H;  // 4 GEMMs
+  printf("bwd_kv B=%d H=%d S=%d D=%d: %.3f ms, %.1f TFLOP/s executed\n", B, H, S, D, ms, fl / (ms * 1e-3) / 1e12);
+  std::vector<unsigned long long> st8(1 << 18);
+  void* dsym;
+  CK(hipGetSymbolAddress(&dsym, HIP_SYMBOL(mfa::g_mfa_bstamps)));
+  CK(hipMemcpy(st8.data(), dsym, sizeof(unsigned long long) << 18, hipMemcpyDeviceToHost));
+  const char* names[8] = {"L/D + DMA issue", "S chain+mask", "dP chain+exp", "dV chain+dS", "dK chain", "wait_vm", "barrier+ld", "prologue"};
+  double tot[8] = {0};
+  int nw = 0;
+  for (size_t w = 0; w < (1 << 15); ++w) {
+    bool any = false;
+    for (int s = 0; s < 8; ++s) any |= st8[w * 8 + s] != 0;
+    if (!any) continue;
+    ++nw;
+    for (int s = 0; s < 8; ++s) tot[s] += (double)st8[w * 8 + s];
+  }
+  double all = 0;
+  for (int s = 0; s < 8; ++s) all += tot[s];
+  const int nsteps = S / (D >= 256 ? 32 : 64);
+  printf("waves %d; per wave per step (shader cycles):\n", nw);
+  for (int s = 0; s < 8; ++s)
+    printf("  %-14s %8.0f  (%.1f%%)\n", names[s], tot[s] / nw / (s == 7 ? 1 : nsteps), 100.0 * tot[s] / all);
+  return 0;
+}
