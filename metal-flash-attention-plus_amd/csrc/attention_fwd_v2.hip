@@ -38,17 +38,35 @@ __device__ unsigned long long g_mfa_stamps[1 << 20];
       g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (slot)] = t_; \
   } while (0)
 #define MFA_STAMP_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+// Shader-cycle phase totals (slots 5..7 of the wave's record).
+#define MFA_ACC_DECL() unsigned long long acc_[3] = {0, 0, 0}, acct_ = __builtin_amdgcn_s_memtime()
+#define MFA_ACC(k)                                                  \
+  do {                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    acc_[k] += t_ - acct_;                                          \
+    acct_ = t_;                                                     \
+  } while (0)
+#define MFA_ACC_END()                                                                      \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) == 0)                                                           \
+      for (int k_ = 0; k_ < 3; ++k_)                                                       \
+        g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 5 + k_] = acc_[k_]; \
+  } while (0)
 #else
+#define MFA_ACC_DECL() do {} while (0)
+#define MFA_ACC(k) do {} while (0)
+#define MFA_ACC_END() do {} while (0)
 #define MFA_STAMP(slot) do {} while (0)
 #define MFA_STAMP_DRAIN() do {} while (0)
 #endif
 
 // Scheduling knobs (development A/B; the defaults are the shipped configuration): fragment
 // read-ahead for the QK^T and PV chains, MFMA-cluster priority, order pinning.
-template <int AHK_ = 4, int AHV_ = 3, bool PRIO_ = false, bool PIN_ = true>
+template <int AHK_ = 4, int AHV_ = 3, bool PRIO_ = false, bool PIN_ = true, bool SPREAD_ = false>
 struct Tune {
   static constexpr int AHK = AHK_, AHV = AHV_;
   static constexpr bool PRIO = PRIO_, PIN = PIN_;
+  static constexpr bool SPREAD = SPREAD_;  // next tile's DMA pieces between the QK^T MFMAs
 };
 using TuneDefault = Tune<>;
 
@@ -72,11 +90,17 @@ struct RowState {
 
 // One BK-key tile for one wave: S^T = K·Q^T (key in registers, query on the lane), masks,
 // online softmax, O^T += V^T·P^T.
-template <class E, int DP, int BK, class TU = TuneDefault>
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+// qk_hook(i) runs after QK^T MFMA i (e.g. staging the next tile piece by piece).
+template <class E, int DP, int BK, class TU = TuneDefault, class QKHook = NoHook>
 __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const int (&rbase)[2],
                                           const int (&trb)[2], const i16x8 (&qf)[DP / 16],
                                           RowState<DP>& st, int t, bool mask_tile, int qi,
-                                          const FwdParams& p, float c, int wsz, int hh) {
+                                          const FwdParams& p, float c, int wsz, int hh,
+                                          QKHook&& qk_hook = QKHook()) {
   using A = Arith16<E, DP>;
   // Pre-scaled Q, S' = S·c − moff from the MFMA (fp16 up to D=128: at D=256 the −m tile's
   // registers are worth more than the per-element multiply-add, which halves per MFMA there).
@@ -99,6 +123,7 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
       else
         s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
       if (i + AH < NM) kf[i % AH] = A::read_row_a(kt, rbase, (i + AH) % NJ, (i + AH) / NJ);
+      qk_hook(i);
       if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
@@ -294,20 +319,38 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   wait_vm();
   __syncthreads();
   MFA_STAMP(1);
+  MFA_ACC_DECL();
 
   int cur = 0;
   for (int t = kbeg; t < kend; t += BK) {
-    if (t + BK < kend) {
+    const bool nxt = t + BK < kend;
+    if (!TU::SPREAD && nxt) {
       kd.issue(khead, t + BK, kb0 + (cur ^ 1) * TILEB);
       vd.issue(vhead, t + BK, vb0 + (cur ^ 1) * TILEB);
     }
+    MFA_ACC(0);
+    auto hook = [&](int i) {
+      if constexpr (TU::SPREAD) {
+        constexpr int PPW = DmaA<DP, BK, NT>::PPW;
+        if ((i & 1) == 0 && i / 2 < 2 * PPW && nxt) {
+          const int k = i / 2;
+          if (k < PPW)
+            kd.issue_piece(khead, t + BK, kb0 + (cur ^ 1) * TILEB, k);
+          else
+            vd.issue_piece(vhead, t + BK, vb0 + (cur ^ 1) * TILEB, k - PPW);
+        }
+      }
+    };
     const bool mask_tile = (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
     fwd2_tile<E, DP, BK, TU>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t, mask_tile,
-                         qi, p, c, wsz, hh);
+                         qi, p, c, wsz, hh, hook);
+    MFA_ACC(1);
     wait_vm();
     __syncthreads();
+    MFA_ACC(2);
     cur ^= 1;
   }
+  MFA_ACC_END();
 
   MFA_STAMP(2);
   float l = cross_half_sum(st.lh) + kFltMin;
@@ -484,6 +527,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
         case '3': return launch_fwd2<F16, 128, 64, 2, Tune<4, 3, true, true>>(p, stream);
         case '4': return launch_fwd2<F16, 128, 128, 2>(p, stream);
         case '5': return launch_fwd2<F16, 128, 64, 2, Tune<2, 2>>(p, stream);
+        case '6': return launch_fwd2<F16, 128, 64, 2, Tune<4, 3, false, true, true>>(p, stream);
         default: break;
       }
     }

@@ -82,6 +82,13 @@ int main(int argc, char** argv) {
     }
   }
   auto set_var = [&](const std::string& v) {
+    if (v[0] == 't') {  // single-block kernel with MFA_FWD2_TUNE=<digit>
+      setenv("MFA_FWD_VARIANT", "s", 1);
+      setenv("MFA_FWD2_TUNE", v.substr(1).c_str(), 1);
+      unsetenv("MFA_FWD_PAIR");
+      return;
+    }
+    unsetenv("MFA_FWD2_TUNE");
     setenv("MFA_FWD_VARIANT", v.substr(0, 1).c_str(), 1);
     if (v.size() > 1) setenv("MFA_FWD_PAIR", v.substr(1).c_str(), 1);
     else unsetenv("MFA_FWD_PAIR");
@@ -149,7 +156,7 @@ int main(int argc, char** argv) {
   }
   // Per XCD (blockIdx % 8): median and max of the main-loop time (slot 1 -> 2) and of the
   // loop end time (slot 2), µs.
-  const int wpb = (var[0] == 'p') ? 8 : 4;  // waves per workgroup of the stamped variant
+  const int wpb = (var[0] == 'p') ? 8 : 4;  // waves per workgroup of the stamped variant  // waves per workgroup of the stamped variant
   for (int x = 0; x < 8; ++x) {
     std::vector<double> lt, le;
     for (int w = 0; w < (1 << 17); ++w) {
@@ -163,6 +170,21 @@ int main(int argc, char** argv) {
     std::sort(le.begin(), le.end());
     printf("xcd %d: loop med %7.2f max %7.2f | loop end med %7.2f max %7.2f (n=%zu)\n", x,
            lt[lt.size() / 2], lt.back(), le[le.size() / 2], le.back(), lt.size());
+  }
+  if (wpb == 4) {
+    // Single-block kernel: shader-cycle totals per wave of DMA issue / tile / wait+barrier.
+    double a[3] = {0, 0, 0};
+    int nw2 = 0;
+    for (int w = 0; w < (1 << 17); ++w) {
+      if (!stamps[w * 8]) continue;
+      ++nw2;
+      for (int k = 0; k < 3; ++k) a[k] += (double)stamps[w * 8 + 5 + k];
+    }
+    const int nt = causal ? 1 : S / 64;
+    const double tot = a[0] + a[1] + a[2];
+    printf("per wave per tile (shader cycles%s): DMA issue %.0f (%.1f%%), tile %.0f (%.1f%%), wait+barrier %.0f (%.1f%%)\n",
+           causal ? ", totals: causal" : "", a[0] / nw2 / nt, 100 * a[0] / tot, a[1] / nw2 / nt,
+           100 * a[1] / tot, a[2] / nw2 / nt, 100 * a[2] / tot);
   }
   return 0;
 }
