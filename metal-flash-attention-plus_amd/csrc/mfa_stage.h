@@ -321,6 +321,27 @@ __device__ __forceinline__ void load_row_frags(typename A::frag (&f)[A::DSTEPS],
 // row & 15, so each wave needs a single lane offset.  Rows past the end and chunks past the
 // row's valid bytes read as zeros: the range-checked descriptor is rebuilt per piece from
 // wave-uniform values (base at the piece's first row, num_records = bytes left).
+// One LDS-DMA wave-instruction: 16 bytes per lane from base + voff (range-checked against
+// nrec bytes; out of range reads zero) into dst + 16*lane.  Issued as inline asm so that
+// hipcc knows nothing of the LDS write: with the builtin it guards later ds_reads with
+// vmcnt(0) (it cannot tell the ring slot being filled from the slot being read), which exposes
+// the prefetch latency every tile; callers order tiles with wait_vm() + a barrier.
+__device__ __forceinline__ void lds_dma16(const void* base, int nrec, int voff, char* dst) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  u32x4 rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);
+  rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
+  rs[3] = 0x00020000u;
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)dst));
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(rs), "s"(lds)
+               : "memory", "m0");
+}
+
 template <int ROWB, int BK, int NT>
 struct TileDMA {
   using T = Tile16<ROWB / 2>;
@@ -350,10 +371,7 @@ struct TileDMA {
     for (int i = 0; i < PPW; ++i) {
       const int n = w + NW * i;
       const int rb = (t + n * RP) * step;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(base + rb), (short)0, max(bytes - rb, 0), 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(dst + n * 1024), 16, off, 0, 0, 0);
+      lds_dma16(base + rb, max(bytes - rb, 0), off, dst + n * 1024);
     }
   }
 };
@@ -395,26 +413,10 @@ struct DmaA {
   }
   // Piece i (< PPW) of this wave's share alone: spread over the MFMAs of a chain, each
   // piece's issue cost hides in an MFMA gap instead of queueing behind the others.
-  // Issued as inline asm: the compiler then knows nothing of the LDS write, so it does not
-  // guard every later ds_read with vmcnt(0) (it cannot tell the slot being filled from the
-  // slot being read); the caller's wait_vm() + barrier order the tile instead.
   __device__ __forceinline__ void issue_piece(const char* head, int t, char* dst, int i) const {
     const int n = w + NW * i;
     const int rb = t * step;
-    const uint64_t base = (uint64_t)(uintptr_t)(head + rb);
-    const int nrec = max(bytes - rb, 0);
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 rs;
-    rs[0] = __builtin_amdgcn_readfirstlane((unsigned)base);
-    rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32) & 0xffffu);
-    rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
-    rs[3] = 0x00020000u;
-    const unsigned lds = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(dst + n * 1024)));
-    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-                 :
-                 : "v"(off[i]), "s"(rs), "s"(lds)
-                 : "memory", "m0");
+    lds_dma16(head + rb, max(bytes - rb, 0), off[i], dst + n * 1024);
   }
 };
 
