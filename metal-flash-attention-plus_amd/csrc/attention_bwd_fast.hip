@@ -31,11 +31,15 @@ namespace mfa {
 // D = 256 backwardKeyValue schedule: softmax work threaded between the MFMAs (true) or the
 // dual-chain schedule with the softmax as one block (false).
 constexpr bool kBwdKv256Interleave = true;
-// backwardKeyValue: stage the next Q/dO tiles piece by piece between the first chain's MFMAs
-// (D = 256: 5.03 vs 5.18 ms at B4 H32 S4096) or all at once at the top of the step (D <= 128:
-// 2.78 vs 3.30 ms; tools/diag/bwd_stamps).
+// backwardKeyValue: stage the next Q/dO tiles all at once at the top of the step (default)
+// or piece by piece between the first chain's MFMAs (development A/B: with the loop's waits
+// fixed the upfront issue is faster at every D, e.g. D=256 B4 H32 S4096 4.26 vs 4.53 ms and
+// D=128 2.40 vs 2.51 ms; tools/diag/bwd_stamps*).
+#ifndef MFA_SPREAD_EVERY
+#define MFA_SPREAD_EVERY 2  // one piece per this many MFMAs of the first chain
+#endif
 #ifndef MFA_SPREAD_MIN_DP
-#define MFA_SPREAD_MIN_DP 256
+#define MFA_SPREAD_MIN_DP 1024
 #endif
 template <int DP>
 constexpr bool spread_dma() { return DP >= MFA_SPREAD_MIN_DP; }
@@ -449,8 +453,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     // chain, so each piece's issue cost sits in an MFMA gap.
     auto dma_hook = [&](int i) {
       constexpr int PPW = DmaA<DP, BQ, NT>::PPW;
-      if (spread_dma<DP>() && (i & 1) == 0 && i / 2 < 2 * PPW && has_next) {
-        const int k = i / 2;
+      constexpr int EVERY = MFA_SPREAD_EVERY;
+      if (spread_dma<DP>() && (i % EVERY) == 0 && i / EVERY < 2 * PPW && has_next) {
+        const int k = i / EVERY;
         if (k < PPW)
           qd.issue_piece(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB, k);
         else
@@ -551,39 +556,39 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       // both chains), then P, then dS threaded through the dV chain.
       dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase, dma_hook);
       apply_mask();
+      BST(1);
+      static_assert(NJ == 1, "D = 256 runs 32-query steps");
+      // P of k-step 0 (registers 0..7) before the dV chain, which needs it first; P of k-step 1
+      // between the chain's first eight MFMAs (they use k-step 0), dS under all sixteen.
+      i16x8 pb[2], sb[2];
+      float lq[4][4];
 #pragma unroll
-      for (int grp = 0; grp < NG; ++grp) {
-        float lq[4];
-        ldg(lt, grp, lq);
+      for (int g4 = 0; g4 < 4; ++g4) ldg(lt, g4, lq[g4]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int idx = grp * 4 + k, jj = idx >> 4, ii = idx & 15;
-          s[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -lq[k]));
-        }
-      }
-      i16x8 pb[NJ * 2], sb[NJ * 2];
-#pragma unroll
-      for (int jk = 0; jk < NJ * 2; ++jk) pb[jk] = A::pack(s[jk >> 1], jk & 1);
+      for (int ii = 0; ii < 8; ++ii)
+        s[0][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[0][ii], c, -lq[ii >> 2][ii & 3]));
+      pb[0] = A::pack(s[0], 0);
+      BST(2);
       {
-        constexpr int NMV = NJ * 2 * ND;
-        constexpr int EPM = (NJ * 16 + NMV - 1) / NMV;
+        constexpr int NMV = 2 * ND;
+        static_assert(NMV == 16, "one dS element per dV MFMA");
         float dq[2][4];
         ldg(dtl, 0, dq[0]);
         tr_chain<A, NJ, ND>(ot, trb, pb, dv, [&](int i) {
-#pragma unroll
-          for (int e = 0; e < EPM; ++e) {
-            const int idx = i * EPM + e;
-            if (idx < NJ * 16) {
-              const int jj = idx >> 4, ii = idx & 15;
-              const int grp = idx >> 2, k = idx & 3;
-              if (k == 0 && grp + 1 < NG) ldg(dtl, grp + 1, dq[(grp + 1) & 1]);
-              dp[jj][ii] = s[jj][ii] * __builtin_fmaf(dp[jj][ii], sc, -dq[grp & 1][k]);
-              if ((ii & 7) == 7) sb[jj * 2 + (ii >> 3)] = A::pack(dp[jj], ii >> 3);
-            }
+          if (i < 8) {
+            const int ii = 8 + i;
+            s[0][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[0][ii], c, -lq[ii >> 2][ii & 3]));
+            if (i == 7) pb[1] = A::pack(s[0], 1);
           }
+          const int ii = i, grp = ii >> 2, k = ii & 3;
+          if (k == 0 && grp + 1 < NG) ldg(dtl, grp + 1, dq[(grp + 1) & 1]);
+          dp[0][ii] = s[0][ii] * __builtin_fmaf(dp[0][ii], sc, -dq[grp & 1][k]);
+          if ((ii & 7) == 7) sb[ii >> 3] = A::pack(dp[0], ii >> 3);
         });
       }
+      BST(3);
       tr_chain<A, NJ, ND>(qt, trb, sb, dk, [](int) {});
+      BST(4);
     } else {
       // D = 256 (previous schedule) runs at the register limit: S and dP chains together, then the softmax, then
       // dV and dK together.

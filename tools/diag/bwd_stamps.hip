@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
   void* dsym;
   CK(hipGetSymbolAddress(&dsym, HIP_SYMBOL(mfa::g_mfa_bstamps)));
   CK(hipMemcpy(st8.data(), dsym, sizeof(unsigned long long) << 18, hipMemcpyDeviceToHost));
-  const char* names[8] = {"L/D + DMA issue", "S chain+mask", "dP chain+exp", "dV chain+dS", "dK chain", "wait_vm", "barrier+ld", "prologue"};
+  const char* names[8] = {"L/D + DMA issue", "S(+dP) chain", "dP chain|P", "dV chain+dS", "dK chain", "wait_vm", "barrier+ld", "prologue"};
   double tot[8] = {0};
   int nw = 0;
   for (size_t w = 0; w < (1 << 15); ++w) {
