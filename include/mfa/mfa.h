@@ -360,12 +360,16 @@ mfa_status_t mfa_dequantize(const mfa_quantized_tensor_t* tensor, uint64_t count
 /* GEMM + MLA (Sources/FlashAttention/GEMM/GEMMDescriptor.swift, Attention/            */
 /* MLAOptimizedGEMMMFA.swift).                                                          */
 
-/* GEMMDescriptor (GEMMDescriptor.swift:11-47): C[M,N] = A[M,K] · B[K,N] (+ C when
- * load_previous_c).  Row-major, leading dimensions default to the packed ones. */
+/* GEMMDescriptor (GEMMDescriptor.swift:11-47): C[M,N] = op(A)·op(B) (+ C when
+ * load_previous_c, GEMMDescriptor.swift:400).  Row-major.  A is [M][K], or [K][M] when
+ * transpose_a; B is [K][N], or [N][K] when transpose_b (GEMMDescriptor.swift:344-372).
+ * Leading dimensions default to the packed ones (0) and must not be smaller than them
+ * ("Leading block dimension was too small.", :359).  Memory precisions FP32 / FP16 / BF16,
+ * chosen independently per operand (AdversarialShapeTest.swift:14-40). */
 typedef struct mfa_gemm_descriptor {
   uint32_t M, N, K;
-  int32_t precision_a, precision_b, precision_c; /* FP16 / BF16 (C may be FP32) */
-  int32_t transpose_a, transpose_b;              /* must be 0 (MLA uses NN) */
+  int32_t precision_a, precision_b, precision_c; /* mfa_precision_t: FP32 / FP16 / BF16 */
+  int32_t transpose_a, transpose_b;
   int32_t load_previous_c;
   uint32_t lda, ldb, ldc;                        /* 0 = packed */
   uint32_t batch;                                /* independent GEMMs (grid z) */
@@ -374,6 +378,28 @@ typedef struct mfa_gemm_descriptor {
 
 mfa_status_t mfa_gemm(const mfa_gemm_descriptor_t* desc, const void* A, const void* B,
                       void* C, void* stream);
+
+/* GEMMKernelDescriptor(descriptor:) + GEMMKernel (GEMMKernelDescriptor.swift:8-60,
+ * GEMMDescriptor.swift:110-246, GEMMKernel.swift): the plan mfa_gemm will run.  Register
+ * precisions follow the gfx950 policy: A and B of one 16-bit type multiply on the 16-bit
+ * matrix core, every other mix in FP32; C always accumulates in FP32 (the reference keeps
+ * FP16 x FP16 -> FP16 in FP16 registers, GEMMDescriptor.swift:204-210). */
+typedef struct mfa_gemm_kernel_descriptor {
+  uint16_t block_m, block_n, block_k;
+  uint16_t splits_m, splits_n;            /* waves along M and N */
+  int32_t memory_precisions[3];           /* A, B, C */
+  int32_t register_precisions[3];         /* A, B, C */
+  int32_t transpose_a, transpose_b;
+  int32_t load_previous_c;
+  uint32_t lda, ldb, ldc;                 /* resolved leading dimensions */
+  uint32_t threadgroup_size;
+  uint32_t threadgroup_memory_allocation; /* LDS bytes per workgroup */
+  uint32_t grid_x, grid_y, grid_z;        /* workgroups along N, M, batch */
+  char variant[64];
+} mfa_gemm_kernel_descriptor_t;
+
+mfa_status_t mfa_gemm_kernel_descriptor(const mfa_gemm_descriptor_t* desc,
+                                        mfa_gemm_kernel_descriptor_t* out);
 
 /* MLAOptimizedGEMMMFA.forward (MLAOptimizedGEMMMFA.swift:158-240) followed by the
  * attention forward the reference's caller runs on the decompressed BSHD K/V
@@ -396,6 +422,29 @@ mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const void* kv_la
                              const void* w_k, const void* w_v, const void* query,
                              void* decompressed_k, void* decompressed_v, float* output,
                              void* logsumexp, void* stream);
+
+/* ---------------------------------------------------------------------------------- */
+/* HadamardRotation (Sources/FlashAttention/Attention/HadamardRotation.swift).           */
+
+/* rotate(buffer:blockSize:numBlocks:) (:43-88): in-place FWHT of every block of an FP32
+ * buffer [num_blocks][block_size] (power of two, <= 1024; buffer 16-byte aligned when
+ * block_size >= 4), then x *= mfa_hadamard_scale(block_size).  Enqueued on `stream`. */
+mfa_status_t mfa_hadamard_rotate(float* buffer, uint32_t block_size, uint32_t num_blocks,
+                                 void* stream);
+
+/* rotateBatch(buffers:) (:91-109): every item validated first, then enqueued in order. */
+typedef struct mfa_hadamard_item {
+  float* buffer;
+  uint32_t block_size;
+  uint32_t num_blocks;
+} mfa_hadamard_item_t;
+mfa_status_t mfa_hadamard_rotate_batch(const mfa_hadamard_item_t* items, uint32_t count,
+                                       void* stream);
+
+/* The normalisation factor: FP32 1/sqrt(block_size), correctly rounded (the reference's
+ * Metal rsqrt, :132, is exact for powers of 4; for odd powers of two its rounding is not
+ * specified). */
+float mfa_hadamard_scale(uint32_t block_size);
 
 /* ---------------------------------------------------------------------------------- */
 /* Host utilities mirrored from the reference.                                          */

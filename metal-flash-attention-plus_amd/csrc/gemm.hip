@@ -9,6 +9,8 @@
 // the same permuted k order (two 8-byte reads per fragment) so the products pair up.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <string.h>
 
 #include "../../include/mfa/mfa.h"
 #include "mfa_device.h"
@@ -318,32 +320,124 @@ template __global__ void mfa_gemm2_kernel<BF16>(GemmParams);
 
 }  // namespace mfa
 
+namespace {
+
+struct GemmPlan {
+  bool tuned;           // NN, equal 16-bit A/B: the kernels above
+  int compute;          // P_FP16 / P_BF16 / P_FP32
+  uint32_t lda, ldb, ldc;
+};
+
+int esize(int prec) { return prec == mfa::P_FP32 ? 4 : 2; }
+bool gemm_prec_ok(int p) {
+  return p == MFA_PRECISION_FP32 || p == MFA_PRECISION_FP16 || p == MFA_PRECISION_BF16;
+}
+
+// Validation and leading-dimension resolution of GEMMDescriptor.setFunctionConstants
+// (GEMMDescriptor.swift:344-372): expected ld = rows when transposed, else columns.
+mfa_status_t gemm_plan(const mfa_gemm_descriptor_t* d, GemmPlan* pl) {
+  if (!gemm_prec_ok(d->precision_a) || !gemm_prec_ok(d->precision_b) ||
+      !gemm_prec_ok(d->precision_c)) {
+    mfa_api_set_error("mfa_gemm: memory precisions must be FP32, FP16 or BF16");
+    return MFA_ERR_UNSUPPORTED;
+  }
+  if (d->M > 0x7fffffffu || d->N > 0x7fffffffu || d->K > 0x7fffffffu) {
+    mfa_api_set_error("mfa_gemm: matrix dimensions exceed 2^31");
+    return MFA_ERR_INVALID_ARGUMENT;
+  }
+  const uint32_t ea = d->transpose_a ? d->M : d->K;
+  const uint32_t eb = d->transpose_b ? d->K : d->N;
+  const uint32_t ec = d->N;
+  pl->lda = d->lda ? d->lda : ea;
+  pl->ldb = d->ldb ? d->ldb : eb;
+  pl->ldc = d->ldc ? d->ldc : ec;
+  if (pl->lda < ea || pl->ldb < eb || pl->ldc < ec) {
+    mfa_api_set_error("mfa_gemm: Leading block dimension was too small.");
+    return MFA_ERR_INVALID_DESCRIPTOR;
+  }
+  pl->compute = mfa::gemm_general_compute(d->precision_a, d->precision_b);
+  pl->tuned = !d->transpose_a && !d->transpose_b && pl->compute != mfa::P_FP32;
+  return MFA_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" mfa_status_t mfa_gemm_kernel_descriptor(const mfa_gemm_descriptor_t* d,
+                                                   mfa_gemm_kernel_descriptor_t* out) {
+  if (!d || !out) return MFA_ERR_INVALID_ARGUMENT;
+  GemmPlan pl;
+  mfa_status_t st = gemm_plan(d, &pl);
+  if (st != MFA_SUCCESS) return st;
+  memset(out, 0, sizeof(*out));
+  out->block_m = 128;
+  out->block_n = 128;
+  out->block_k = pl.compute == mfa::P_FP32 ? 16 : 32;
+  out->splits_m = 2;
+  out->splits_n = 2;
+  out->memory_precisions[0] = d->precision_a;
+  out->memory_precisions[1] = d->precision_b;
+  out->memory_precisions[2] = d->precision_c;
+  out->register_precisions[0] = pl.compute;
+  out->register_precisions[1] = pl.compute;
+  out->register_precisions[2] = MFA_PRECISION_FP32;
+  out->transpose_a = d->transpose_a;
+  out->transpose_b = d->transpose_b;
+  out->load_previous_c = d->load_previous_c;
+  out->lda = pl.lda; out->ldb = pl.ldb; out->ldc = pl.ldc;
+  out->threadgroup_size = 256;
+  out->grid_x = (d->N + 127) / 128;
+  out->grid_y = (d->M + 127) / 128;
+  out->grid_z = d->batch ? d->batch : 1;
+  const char* cn = pl.compute == mfa::P_FP16 ? "f16" : pl.compute == mfa::P_BF16 ? "bf16" : "f32";
+  if (pl.tuned) {
+    out->threadgroup_memory_allocation = 2 * (128 * 32 * 2 + 32 * 128 * 2);
+    snprintf(out->variant, sizeof(out->variant), "mfa_gemm_kernel<%s>/mfa_gemm2_kernel<%s>", cn, cn);
+  } else {
+    out->threadgroup_memory_allocation = 4 * 128 * 64;
+    snprintf(out->variant, sizeof(out->variant), "mfa_gemm_general_kernel<%s,%s%s>", cn,
+             d->transpose_a ? "T" : "N", d->transpose_b ? "T" : "N");
+  }
+  return MFA_SUCCESS;
+}
+
 extern "C" mfa_status_t mfa_gemm(const mfa_gemm_descriptor_t* d, const void* A, const void* B,
                                  void* C, void* stream) {
   using namespace mfa;
   if (!d || !A || !B || !C) return MFA_ERR_INVALID_ARGUMENT;
-  if (d->transpose_a || d->transpose_b) return MFA_ERR_UNSUPPORTED;
-  if (d->precision_a != d->precision_b ||
-      (d->precision_a != MFA_PRECISION_FP16 && d->precision_a != MFA_PRECISION_BF16))
-    return MFA_ERR_UNSUPPORTED;
-  if (d->precision_c != MFA_PRECISION_FP32 && d->precision_c != MFA_PRECISION_FP16 &&
-      d->precision_c != MFA_PRECISION_BF16)
-    return MFA_ERR_UNSUPPORTED;
+  GemmPlan pl;
+  mfa_status_t st = gemm_plan(d, &pl);
+  if (st != MFA_SUCCESS) return st;
   if (d->M == 0 || d->N == 0) return MFA_SUCCESS;
-  GemmParams p{};
-  p.a = A;
-  p.b[0] = B;
-  p.b[1] = nullptr;
-  p.c[0] = C;
-  p.M = (int)d->M; p.N = (int)d->N; p.K = (int)d->K;
-  p.lda = d->lda ? (int)d->lda : (int)d->K;
-  p.ldb = d->ldb ? (int)d->ldb : (int)d->N;
-  p.ldc = d->ldc ? (int)d->ldc : (int)d->N;
-  p.sa = (int64_t)d->stride_a; p.sb = (int64_t)d->stride_b; p.sc = (int64_t)d->stride_c;
-  p.prec_c = d->precision_c;
-  p.load_prev = d->load_previous_c;
   const int batch = d->batch ? (int)d->batch : 1;
-  return gemm_dispatch(p, d->precision_a, batch, (hipStream_t)stream) == hipSuccess
-             ? MFA_SUCCESS
-             : MFA_ERR_LAUNCH;
+  hipError_t e;
+  if (pl.tuned) {
+    GemmParams p{};
+    p.a = A;
+    p.b[0] = B;
+    p.b[1] = nullptr;
+    p.c[0] = C;
+    p.M = (int)d->M; p.N = (int)d->N; p.K = (int)d->K;
+    p.lda = (int)pl.lda; p.ldb = (int)pl.ldb; p.ldc = (int)pl.ldc;
+    p.sa = (int64_t)d->stride_a; p.sb = (int64_t)d->stride_b; p.sc = (int64_t)d->stride_c;
+    p.prec_c = d->precision_c;
+    p.load_prev = d->load_previous_c;
+    e = gemm_dispatch(p, d->precision_a, batch, (hipStream_t)stream);
+  } else {
+    GemmGParams p{};
+    p.a = A; p.b = B; p.c = C;
+    p.M = (int)d->M; p.N = (int)d->N; p.K = (int)d->K;
+    p.lda = (int)pl.lda; p.ldb = (int)pl.ldb; p.ldc = (int)pl.ldc;
+    p.sa = (int64_t)d->stride_a; p.sb = (int64_t)d->stride_b; p.sc = (int64_t)d->stride_c;
+    p.prec_a = d->precision_a; p.prec_b = d->precision_b; p.prec_c = d->precision_c;
+    p.esz_a = esize(p.prec_a); p.esz_b = esize(p.prec_b); p.esz_c = esize(p.prec_c);
+    p.trans_a = d->transpose_a ? 1 : 0;
+    p.trans_b = d->transpose_b ? 1 : 0;
+    p.load_prev = d->load_previous_c;
+    e = gemm_general_dispatch(p, batch, (hipStream_t)stream);
+  }
+  if (e != hipSuccess) {
+    mfa_api_set_error("mfa_gemm: kernel launch failed");
+    return MFA_ERR_LAUNCH;
+  }
+  return MFA_SUCCESS;
 }

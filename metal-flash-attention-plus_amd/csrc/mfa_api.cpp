@@ -268,11 +268,17 @@ float resolve_scale(const mfa_attention_descriptor_t& d, int head_dim) {
 
 }  // namespace
 
+void mfa_api_set_error(const char* msg) {
+  g_last_error = msg;
+  if (getenv("MFA_DEBUG")) fprintf(stderr, "[mfa] %s\n", msg);
+}
+
 // =========================================================================================
 extern "C" {
 
 const char* mfa_version(void) { return "mfa-cdna4 0.1.0 (gfx950)"; }
 const char* mfa_last_error(void) { return g_last_error.c_str(); }
+
 int mfa_abi_version(void) { return MFA_ABI_VERSION; }
 
 int mfa_operand_buffer_binding(mfa_operand_t operand) {

@@ -75,4 +75,18 @@ struct GemmParams {
   int32_t load_prev;
 };
 
+// General GEMM (gemm_general.hip): any FP32/FP16/BF16 mix, transposes, leading dimensions.
+struct GemmGParams {
+  const void* a;
+  const void* b;
+  void* c;
+  int32_t M, N, K;
+  int32_t lda, ldb, ldc;
+  int64_t sa, sb, sc;       // batch strides (elements)
+  int32_t prec_a, prec_b, prec_c;
+  int32_t esz_a, esz_b, esz_c;
+  int32_t trans_a, trans_b;
+  int32_t load_prev;
+};
+
 }  // namespace mfa

@@ -312,6 +312,22 @@ class GemmDescriptor(ctypes.Structure):
     ]
 
 
+class GemmKernelDescriptor(ctypes.Structure):  # GEMMKernelDescriptor.swift:8-60
+    _fields_ = [
+        ("block_m", ctypes.c_uint16), ("block_n", ctypes.c_uint16), ("block_k", ctypes.c_uint16),
+        ("splits_m", ctypes.c_uint16), ("splits_n", ctypes.c_uint16),
+        ("memory_precisions", ctypes.c_int32 * 3),
+        ("register_precisions", ctypes.c_int32 * 3),
+        ("transpose_a", ctypes.c_int32), ("transpose_b", ctypes.c_int32),
+        ("load_previous_c", ctypes.c_int32),
+        ("lda", ctypes.c_uint32), ("ldb", ctypes.c_uint32), ("ldc", ctypes.c_uint32),
+        ("threadgroup_size", ctypes.c_uint32),
+        ("threadgroup_memory_allocation", ctypes.c_uint32),
+        ("grid_x", ctypes.c_uint32), ("grid_y", ctypes.c_uint32), ("grid_z", ctypes.c_uint32),
+        ("variant", ctypes.c_char * 64),
+    ]
+
+
 class MLADescriptor(ctypes.Structure):
     _fields_ = [
         ("base", AttentionDescriptor),
@@ -365,8 +381,12 @@ _sig("mfa_quantize", ctypes.c_int,
 _sig("mfa_dequantize", ctypes.c_int,
      [_P(QuantizedTensor), ctypes.c_uint64, ctypes.c_uint32, _V, _V])
 _sig("mfa_gemm", ctypes.c_int, [_P(GemmDescriptor), _V, _V, _V, _V])
+_sig("mfa_gemm_kernel_descriptor", ctypes.c_int, [_P(GemmDescriptor), _P(GemmKernelDescriptor)])
 _sig("mfa_mla_forward", ctypes.c_int,
      [_P(MLADescriptor), _V, _V, _V, _V, _V, _V, _V, _V, _V])
+_sig("mfa_hadamard_rotate", ctypes.c_int, [_V, ctypes.c_uint32, ctypes.c_uint32, _V])
+_sig("mfa_hadamard_rotate_batch", ctypes.c_int, [_V, ctypes.c_uint32, _V])
+_sig("mfa_hadamard_scale", ctypes.c_float, [ctypes.c_uint32])
 _sig("mfa_masking_sequence_bucket", ctypes.c_int, [ctypes.c_int])
 _sig("mfa_masking_default_rule", ctypes.c_int, [ctypes.c_int, ctypes.c_int])
 _sig("mfa_sparse_build_sliding_window", None, [ctypes.c_uint32, ctypes.c_uint32, _V])
@@ -536,16 +556,69 @@ def quantize(x, target: Precision, mode: QuantMode = QuantMode.tensorWise, rows=
     return data, scale, (bs if nb else None), (bz if nb else None)
 
 
-def gemm(A, B, C, M, N, K, prec_a: Precision, prec_c: Precision, load_previous_c=False,
-         stream=None, batch=1, stride_a=0, stride_b=0, stride_c=0):
+def gemm_descriptor(M, N, K, prec_a: Precision, prec_c: Precision, prec_b=None,
+                    transpose_a=False, transpose_b=False, lda=0, ldb=0, ldc=0,
+                    load_previous_c=False, batch=1, stride_a=0, stride_b=0, stride_c=0):
+    """GEMMDescriptor (GEMMDescriptor.swift:11-47) as the C struct; prec_b defaults to prec_a."""
     d = GemmDescriptor()
     d.M, d.N, d.K = M, N, K
-    d.precision_a = d.precision_b = int(prec_a)
+    d.precision_a = int(prec_a)
+    d.precision_b = int(prec_a if prec_b is None else prec_b)
     d.precision_c = int(prec_c)
+    d.transpose_a, d.transpose_b = int(bool(transpose_a)), int(bool(transpose_b))
+    d.lda, d.ldb, d.ldc = lda, ldb, ldc
     d.load_previous_c = int(load_previous_c)
     d.batch = batch
     d.stride_a, d.stride_b, d.stride_c = stride_a, stride_b, stride_c
+    return d
+
+
+def gemm_kernel_descriptor(d: GemmDescriptor) -> GemmKernelDescriptor:
+    """GEMMKernelDescriptor(descriptor:) (GEMMDescriptor.swift:110-246): the plan mfa_gemm runs."""
+    out = GemmKernelDescriptor()
+    check(lib.mfa_gemm_kernel_descriptor(ctypes.byref(d), ctypes.byref(out)))
+    return out
+
+
+def gemm(A, B, C, M, N, K, prec_a: Precision, prec_c: Precision, load_previous_c=False,
+         stream=None, batch=1, stride_a=0, stride_b=0, stride_c=0, prec_b=None,
+         transpose_a=False, transpose_b=False, lda=0, ldb=0, ldc=0):
+    """C = op(A)·op(B) (+ C): GEMMKernel encode of a GEMMDescriptor (GEMMKernel+Source.swift)."""
+    d = gemm_descriptor(M, N, K, prec_a, prec_c, prec_b, transpose_a, transpose_b, lda, ldb, ldc,
+                        load_previous_c, batch, stride_a, stride_b, stride_c)
     check(lib.mfa_gemm(ctypes.byref(d), _ptr(A), _ptr(B), _ptr(C), _stream(stream)))
+
+
+class HadamardItem(ctypes.Structure):  # rotateBatch tuple (HadamardRotation.swift:91-95)
+    _fields_ = [("buffer", ctypes.c_void_p), ("block_size", ctypes.c_uint32),
+                ("num_blocks", ctypes.c_uint32)]
+
+
+class HadamardRotation:
+    """HadamardRotation (Attention/HadamardRotation.swift:22-180): group-wise FWHT of FP32
+    device buffers [num_blocks, block_size], in place, on the HIP kernel."""
+
+    def rotate(self, buffer, block_size: int, num_blocks: int, stream=None):
+        import torch
+        if buffer.dtype != torch.float32:
+            raise MFAError(4, "HadamardRotation.rotate: the buffer must be FP32")
+        if buffer.numel() < block_size * num_blocks:
+            raise MFAError(4, "HadamardRotation.rotate: buffer smaller than blockSize * numBlocks")
+        check(lib.mfa_hadamard_rotate(_ptr(buffer), block_size, num_blocks, _stream(stream)))
+        return buffer
+
+    def rotate_batch(self, items, stream=None):
+        import torch
+        arr = (HadamardItem * max(len(items), 1))()
+        for i, (buf, bs, nb) in enumerate(items):
+            if buf.dtype != torch.float32 or buf.numel() < bs * nb:
+                raise MFAError(4, "HadamardRotation.rotateBatch: bad buffer")
+            arr[i] = HadamardItem(buf.data_ptr(), bs, nb)
+        check(lib.mfa_hadamard_rotate_batch(arr, len(items), _stream(stream)))
+
+    @staticmethod
+    def scale(block_size: int) -> float:
+        return float(lib.mfa_hadamard_scale(block_size))
 
 
 def mla_forward(base: AttentionDescriptor, kv_latent, w_k, w_v, query, output, B, H, S_q, S_kv,

@@ -485,6 +485,27 @@ ORACLE_API void mfa_oracle_gemm(const float* A, const float* B, float* C, int M,
   }
 }
 
+/* HadamardRotation.swift:111-136 (the MSL kernel hadamard_rotate), one block after another:
+ * stage s pairs elements 2^s apart, (a, b) -> (a + b, a - b); then x *= scale, scale being
+ * the FP32 1/sqrt(N) (see mfa_hadamard_scale in include/mfa/mfa.h). */
+ORACLE_API void mfa_oracle_hadamard(float* data, int block_size, int64_t num_blocks, float scale) {
+  int log2n = 0;
+  while ((1 << log2n) < block_size) ++log2n;
+  for (int64_t g = 0; g < num_blocks; ++g) {
+    float* block = data + g * block_size;
+    for (int s = 0; s < log2n; ++s) {
+      const int stride = 1 << s, pair = stride * 2;
+      for (int i = 0; i < block_size; i += pair)
+        for (int j = 0; j < stride; ++j) {
+          const float a = block[i + j], b = block[i + j + stride];
+          block[i + j] = a + b;
+          block[i + j + stride] = a - b;
+        }
+    }
+    for (int i = 0; i < block_size; ++i) block[i] *= scale;
+  }
+}
+
 /* ---------------------------------------------------------------- CPU baseline */
 
 /* Threads the oracle may use (bench.py's cpu_baseline reports it as `cores`). */

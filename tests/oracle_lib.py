@@ -205,15 +205,30 @@ def dequantize_block(q: np.ndarray, count: int, cols: int, bs: int, prec: int,
     return out
 
 
-def gemm(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+def gemm(A: np.ndarray, B: np.ndarray, prev: np.ndarray | None = None) -> np.ndarray:
+    """C = A·B (+ prev, loadPreviousC) with double accumulation, one fp32 rounding."""
     A = np.ascontiguousarray(A, dtype=np.float32)
     B = np.ascontiguousarray(B, dtype=np.float32)
     M, K = A.shape
     N = B.shape[1]
-    C = np.zeros((M, N), dtype=np.float32)
-    olib.mfa_oracle_gemm(A, B, C, M, N, K, 0)
+    if prev is None:
+        C = np.zeros((M, N), dtype=np.float32)
+    else:
+        C = np.array(prev, dtype=np.float32, copy=True, order="C")
+    olib.mfa_oracle_gemm(A, B, C, M, N, K, 0 if prev is None else 1)
     return C
 
 
 def set_threads(n: int) -> int:
     return int(olib.mfa_oracle_set_threads(n))
+
+
+olib.mfa_oracle_hadamard.argtypes = [_f32p, ctypes.c_int, ctypes.c_int64, ctypes.c_float]
+olib.mfa_oracle_hadamard.restype = None
+
+
+def hadamard(x: np.ndarray, block_size: int, scale: float) -> np.ndarray:
+    """HadamardRotation.rotate on a copy of the flat FP32 buffer x (oracle/mfa_oracle.c)."""
+    y = np.array(x, dtype=np.float32, copy=True, order="C").ravel()
+    olib.mfa_oracle_hadamard(y, block_size, y.size // block_size, scale)
+    return y.reshape(np.shape(x))
