@@ -423,6 +423,19 @@ mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const void* kv_la
                              void* decompressed_k, void* decompressed_v, float* output,
                              void* logsumexp, void* stream);
 
+/* Absorbed MLA (the fused form of MLAOptimizedGEMMMFA.forward,
+ * MLAOptimizedGEMMMFA.swift:213-239): attends in the latent space instead of materialising
+ * K/V — Q̃_h = Q_h·W_k,hᵀ, Õ_h = softmax(scale·Q̃_h·latentᵀ)·latent, O_h = Õ_h·W_v,h — with
+ * scale = softmax_scale of the base descriptor or 1/sqrt(head_dim).  Same arguments and
+ * layouts as mfa_mla_forward; kv_latent_dim must be 256 or 512; masks: none or causal.
+ * `workspace` (nullable → library-owned) holds Q̃ and Õ:
+ * mfa_mla_absorbed_workspace_size() bytes. */
+size_t mfa_mla_absorbed_workspace_size(const mfa_mla_descriptor_t* desc);
+mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* desc, const void* kv_latent,
+                                      const void* w_k, const void* w_v, const void* query,
+                                      void* workspace, float* output, void* logsumexp,
+                                      void* stream);
+
 /* ---------------------------------------------------------------------------------- */
 /* HadamardRotation (Sources/FlashAttention/Attention/HadamardRotation.swift).           */
 

@@ -1,0 +1,295 @@
+// attention_mla_latent.hip — attention in the MLA latent space (the absorbed form of
+// MLAOptimizedGEMMMFA, MLAOptimizedGEMMMFA.swift:158-240).
+//
+// The decompress path computes K_h = latent·W_k,h and V_h = latent·W_v,h, then attends per
+// head.  Since Q_h·K_hᵀ = (Q_h·W_k,hᵀ)·latentᵀ and P·V_h = (P·latent)·W_v,h, the same result
+// comes from
+//     Q̃_h = Q_h·W_k,hᵀ                        (general GEMM, B transposed)
+//     Õ_h = softmax(scale·Q̃_h·latentᵀ)·latent (this kernel: every head attends to ONE
+//                                               [S_kv, LAT] latent, used as both K and V)
+//     O_h = Õ_h·W_v,h                          (16-bit GEMM)
+// with the softmax scale of the decompressed head dimension.  K/V are never materialised;
+// the latent is read once per query block instead of two [S_kv, H·D] tensors.
+//
+// Kernel structure: all heads share the latent, so query rows of every head of a batch item
+// are one flattened [H·S_q, LAT] problem (MQA with a single KV head).  A workgroup is 4 waves
+// on 32 query rows; wave w owns latent dims [w·LAT/4, (w+1)·LAT/4) of both products:
+//   * Sᵀ_w = latent[:, slice]·Q̃[:, slice]ᵀ on MFMA (key on the register, query on the lane),
+//   * the four partial Sᵀ are summed through LDS (fixed order, so every wave holds the same
+//     bits and runs the same online softmax),
+//   * Õᵀ_w += latent[:, slice]ᵀ·Pᵀ with the latent tile read transposed (ds_read_b64_tr_b16).
+// MFMA work is not duplicated; the cost is the partial-S exchange (16 KiB of LDS per tile).
+// Latent tiles of 32 keys are register-staged into a double-buffered [32][LAT] LDS image.
+// Softmax semantics are the reference forward's (AttentionKernel+Softmax.swift:641-892):
+// base-2 online softmax, masked keys at (0.875/log2 e)·(−FLT_MAX) (causal) or −inf (past S_kv),
+// L = m + log2 l.  Õ is written in the 16-bit element type for the final 16-bit GEMM.
+#include "mfa_stage.h"
+#include "mfa_dispatch.h"
+
+namespace mfa {
+
+template <class E, int LAT>
+__global__ void __launch_bounds__(256, 2) mfa_mla_latent_kernel(LatentParams p) {
+  constexpr int BK = 32, NT = 256;
+  constexpr int WS = LAT / 4;              // latent dims per wave
+  constexpr int DS = WS / 16;              // MFMA k-steps of the wave's QK^T slice
+  constexpr int ND = WS / 32;              // O^T tiles per wave
+  constexpr int CPR = LAT / 8;             // 16-byte chunks per latent row
+  constexpr int CPT = BK * CPR / NT;       // chunks staged per thread
+  constexpr int TILEB = BK * LAT * 2;
+  using A = Arith16<E, LAT>;
+  using TT = Tile16<LAT>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const tb0 = smem;                              // 2 latent tiles
+  float* const xb = reinterpret_cast<float*>(smem + 2 * TILEB);  // [4 waves][16][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % p.nsplit;
+  const int bq = blockIdx.x / p.nsplit;
+  const int b = bq / p.nblk;
+  const int r0 = (bq % p.nblk) * 32;
+  const int r = r0 + l32;
+  const bool rvalid = r < p.R;
+  const int spos = rvalid ? r % p.Sq : 0;   // query position of the row (causal)
+
+  // Keys this block needs: all of S_kv, or up to the largest query position it holds.
+  int kend = p.Skv;
+  if (p.causal) {
+    const int rl = min(r0 + 31, p.R - 1);
+    const int smax = (r0 / p.Sq == rl / p.Sq) ? rl % p.Sq : p.Sq - 1;
+    kend = min(kend, smax + 1);
+  }
+  const int kbeg = split * p.chunk;
+  kend = min(kend, kbeg + p.chunk);
+
+  // Q̃ fragments of the wave's slice: d = w·WS + 16·ds + 8·hh + j.
+  i16x8 qf[DS];
+  {
+    const uint16_t* qrow = (const uint16_t*)p.q + ((int64_t)b * p.R + (rvalid ? r : 0)) * LAT;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (rvalid) v = *reinterpret_cast<const i16x8*>(qrow + wave * WS + 16 * ds + 8 * hh);
+      qf[ds] = v;
+    }
+  }
+
+  const uint16_t* lat = (const uint16_t*)p.lat + (int64_t)b * p.Skv * LAT;
+  uint4 stg[CPT];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int id = tid + NT * i;
+      const int row = id / CPR, ch = id % CPR;
+      stg[i] = (t + row < p.Skv)
+                   ? *reinterpret_cast<const uint4*>(lat + (int64_t)(t + row) * LAT + 8 * ch)
+                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto store = [&](char* tile) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int id = tid + NT * i;
+      *reinterpret_cast<uint4*>(tile + TT::off(id / CPR, id % CPR)) = stg[i];
+    }
+  };
+
+  f32x16 o[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) o[dt] = zero16();
+  float m = -kFltMax, lh = 0.f;
+  const float c = p.c_log2;
+
+  if (kbeg < kend) {
+    load(kbeg);
+    store(tb0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int t = kbeg; t < kend; t += BK) {
+    const bool has_next = t + BK < kend;
+    if (has_next) load(t + BK);
+    const char* kt = tb0 + cur * TILEB;
+
+    // Partial S^T over this wave's latent slice.
+    f32x16 sp = zero16();
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds)
+      sp = A::mma(A::read_row(kt, l32, wave * DS + ds, hh), qf[ds], sp);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) xb[(wave * 16 + i) * 64 + lane] = sp[i];
+    __syncthreads();
+    f32x16 s;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      s[i] = ((xb[i * 64 + lane] + xb[(16 + i) * 64 + lane]) + xb[(32 + i) * 64 + lane]) +
+             xb[(48 + i) * 64 + lane];
+
+    if (t + BK > p.Skv || (p.causal && t + BK - 1 > spos)) {
+      MFA_KEEP_BRANCH();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = t + acc_row(i, hh);
+        if (p.causal && key > spos) s[i] = kMaskValue;
+        if (key >= p.Skv) s[i] = -__builtin_inff();
+      }
+    }
+    float mx = s[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
+    const float m_tile = cross_half_max(mx) * c;
+    if (m_tile > m) {
+      const float corr = __builtin_amdgcn_exp2f(m - m_tile);
+      m = m_tile;
+      lh *= corr;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= corr;
+    }
+    float rs = 0.f;
+    if (m < kMaskLevel) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s[i] = __builtin_amdgcn_exp2f(mul_rn(s[i], c) - m);
+        rs += s[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], c, -m));
+        rs += s[i];
+      }
+    }
+    lh += rs;
+    // O^T += latent[:, slice]^T · P^T
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const i16x8 pb = A::pack(s, ks);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+        o[dt] = A::mma(A::read_tr(kt, 0, ks, wave * WS + 32 * dt, lane), pb, o[dt]);
+    }
+    if (has_next) store(tb0 + (cur ^ 1) * TILEB);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  if (p.nsplit > 1) {
+    // Partial state of this key split: Õ unnormalised, (m, l) for the merge pass.
+    const float lp = cross_half_sum(lh);
+    if (!rvalid) return;
+    const int64_t prow = ((int64_t)b * p.nsplit + split) * p.R + r;
+    float* op = p.opart + prow * LAT + wave * WS;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(op + dt * 32 + 8 * g + 4 * hh) =
+            make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
+    if (wave == 0 && hh == 0) p.mlpart[prow] = make_float2(m, lp);
+    return;
+  }
+  float l = cross_half_sum(lh) + kFltMin;
+  if (!(l > 0.f)) l = kFltMin;
+  if (!rvalid) return;
+  const float inv = 1.f / l;
+  uint16_t* orow = (uint16_t*)p.olat + ((int64_t)b * p.R + r) * LAT + wave * WS;
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = dt * 32 + 8 * g + 4 * hh;
+      ushort4 v;
+      v.x = E::from_f32(o[dt][4 * g] * inv);
+      v.y = E::from_f32(o[dt][4 * g + 1] * inv);
+      v.z = E::from_f32(o[dt][4 * g + 2] * inv);
+      v.w = E::from_f32(o[dt][4 * g + 3] * inv);
+      *reinterpret_cast<ushort4*>(orow + d) = v;
+    }
+  if (wave == 0 && hh == 0 && p.l) {
+    const float L = m + __log2f(l);
+    const int64_t li = (int64_t)b * p.R + r;
+    if (p.l_f16)
+      reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+    else
+      reinterpret_cast<float*>(p.l)[li] = L;
+  }
+}
+
+// Merge of the key splits (flash-decoding): M = max m_s, w_s = exp2(m_s − M),
+// Õ = Σ w_s Õ_s / Σ w_s l_s, L = M + log2 Σ w_s l_s.  One workgroup of LAT/4 threads per row.
+template <class E, int LAT>
+__global__ void __launch_bounds__(LAT / 4) mfa_mla_latent_merge_kernel(LatentParams p) {
+  const int64_t row = blockIdx.x;             // b·R + r
+  const int b = (int)(row / p.R), r = (int)(row % p.R);
+  const int d = 4 * threadIdx.x;
+  float M = -kFltMax;
+  for (int s = 0; s < p.nsplit; ++s)
+    M = fmaxf(M, p.mlpart[((int64_t)b * p.nsplit + s) * p.R + r].x);
+  float l = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < p.nsplit; ++s) {
+    const int64_t prow = ((int64_t)b * p.nsplit + s) * p.R + r;
+    const float2 ml = p.mlpart[prow];
+    const float w = __builtin_amdgcn_exp2f(ml.x - M);
+    l += w * ml.y;
+    const float4 x = *reinterpret_cast<const float4*>(p.opart + prow * LAT + d);
+    acc.x += w * x.x; acc.y += w * x.y; acc.z += w * x.z; acc.w += w * x.w;
+  }
+  l += kFltMin;
+  if (!(l > 0.f)) l = kFltMin;
+  const float inv = 1.f / l;
+  ushort4 v;
+  v.x = E::from_f32(acc.x * inv);
+  v.y = E::from_f32(acc.y * inv);
+  v.z = E::from_f32(acc.z * inv);
+  v.w = E::from_f32(acc.w * inv);
+  *reinterpret_cast<ushort4*>((uint16_t*)p.olat + row * LAT + d) = v;
+  if (threadIdx.x == 0 && p.l) {
+    const float L = M + __log2f(l);
+    if (p.l_f16)
+      reinterpret_cast<uint16_t*>(p.l)[row] = f32_to_f16(L);
+    else
+      reinterpret_cast<float*>(p.l)[row] = L;
+  }
+}
+
+template <class E, int LAT>
+static hipError_t launch_latent(const LatentParams& p, hipStream_t stream) {
+  constexpr int LDS = 2 * 32 * LAT * 2 + 4 * 16 * 64 * 4;
+  auto kern = mfa_mla_latent_kernel<E, LAT>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.nsplit), dim3(256), LDS, stream, p);
+  if (p.nsplit > 1) {
+    auto merge = mfa_mla_latent_merge_kernel<E, LAT>;
+    hipLaunchKernelGGL(merge, dim3(p.B * p.R), dim3(LAT / 4), 0, stream, p);
+  }
+  return hipGetLastError();
+}
+
+hipError_t mla_latent_dispatch(const LatentParams& p, int elem, int lat, hipStream_t stream) {
+  if (lat == 512 && elem == P_FP16) return launch_latent<F16, 512>(p, stream);
+  if (lat == 512 && elem == P_BF16) return launch_latent<BF16, 512>(p, stream);
+  if (lat == 256 && elem == P_FP16) return launch_latent<F16, 256>(p, stream);
+  if (lat == 256 && elem == P_BF16) return launch_latent<BF16, 256>(p, stream);
+  return hipErrorNotSupported;
+}
+
+template __global__ void mfa_mla_latent_kernel<F16, 512>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<F16, 512>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<BF16, 512>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<F16, 256>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<BF16, 256>(LatentParams);
+template __global__ void mfa_mla_latent_kernel<BF16, 512>(LatentParams);
+template __global__ void mfa_mla_latent_kernel<F16, 256>(LatentParams);
+template __global__ void mfa_mla_latent_kernel<BF16, 256>(LatentParams);
+
+}  // namespace mfa

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) mfa_gemm_general_kernel(GemmGParams p) {
 
   const int z = blockIdx.z;
   const char* A = (const char*)p.a + (int64_t)z * p.sa * p.esz_a;
-  const char* B = (const char*)p.b + (int64_t)z * p.sb * p.esz_b;
+  const char* B = (const char*)p.b + (int64_t)(p.bmod ? z % p.bmod : z) * p.sb * p.esz_b;
   char* C = (char*)p.c + (int64_t)z * p.sc * p.esz_c;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -978,3 +978,133 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
   if ((st = plan_masks(desc->base, nullptr, Sq, Skv, &p.mask)) != MFA_SUCCESS) return st;
   return hip_status(launch_forward(p, elem, DP, 0, s), "mfa_fwd (MLA) launch");
 }
+
+// =========================================================================================
+// Absorbed MLA: attention in the latent space, K/V never materialised.
+// Q̃ = Q·W_kᵀ per head (general GEMM, B transposed), latent-space attention
+// (attention_mla_latent.hip), O = Õ·W_v per head (16-bit GEMM).  Same result as
+// mfa_mla_forward up to the rounding of Q̃ and Õ to the 16-bit precision (where the
+// decompress path rounds K and V).
+extern "C" size_t mfa_mla_absorbed_workspace_size(const mfa_mla_descriptor_t* desc) {
+  if (!desc) return 0;
+  return (size_t)2 * desc->batch_size * desc->num_heads * desc->sequence_length_q *
+         desc->kv_latent_dim * 2;
+}
+
+extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* desc,
+                                                 const void* kv_latent, const void* w_k,
+                                                 const void* w_v, const void* query,
+                                                 void* workspace, float* output,
+                                                 void* logsumexp, void* stream) {
+  if (!desc || !kv_latent || !w_k || !w_v || !query || !output)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "MLA forward requires latent, weights, query, output");
+  const int prec = desc->precision;
+  if (prec != MFA_PRECISION_FP16 && prec != MFA_PRECISION_BF16)
+    return fail(MFA_ERR_UNSUPPORTED, "MLA precision must be FP16 or BF16");
+  const int B = (int)desc->batch_size, H = (int)desc->num_heads;
+  const int Sq = (int)desc->sequence_length_q, Skv = (int)desc->sequence_length_kv;
+  const int D = (int)desc->head_dim, Lat = (int)desc->kv_latent_dim;
+  if (B <= 0 || H <= 0 || D <= 0 || Lat <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "empty MLA shape");
+  if (Lat != 256 && Lat != 512)
+    return fail(MFA_ERR_UNSUPPORTED, "absorbed MLA needs a latent dimension of 256 or 512 (got %d)", Lat);
+  const int sp = desc->base.sparsity_pattern;
+  if (sp != MFA_SPARSITY_NONE && sp != MFA_SPARSITY_CAUSAL)
+    return fail(MFA_ERR_UNSUPPORTED, "absorbed MLA supports no mask or causal");
+  if (Sq == 0) return MFA_SUCCESS;
+  hipStream_t s = (hipStream_t)stream;
+  mfa_status_t st;
+  const int64_t qlat = (int64_t)B * H * Sq * Lat;  // elements of Q̃ (and of Õ)
+  void* ws = workspace;
+  if (!ws && (st = scratch((size_t)qlat * 2 * 2, &ws, 2)) != MFA_SUCCESS) return st;
+  char* qt = (char*)ws;
+  char* ot = qt + qlat * 2;
+  // One launch per GEMM over all (b, h): W_k / W_v slices depend on h only (bmod = H).
+  auto general = [&](const void* a, const void* w, void* c, int M, int N, int K, int lda,
+                     int ldc, int trans_b, int prec_c, int64_t sa, int64_t sc) {
+    mfa::GemmGParams g;
+    memset(&g, 0, sizeof(g));
+    g.a = a; g.b = w; g.c = c;
+    g.M = M; g.N = N; g.K = K;
+    g.lda = lda; g.ldb = H * D; g.ldc = ldc;
+    g.sa = sa; g.sb = D; g.sc = sc;
+    g.prec_a = g.prec_b = prec; g.prec_c = prec_c;
+    g.esz_a = g.esz_b = 2; g.esz_c = prec_c == MFA_PRECISION_FP32 ? 4 : 2;
+    g.trans_b = trans_b;
+    g.bmod = H;
+    return hip_status(mfa::gemm_general_dispatch(g, B * H, s), "absorbed MLA GEMM launch");
+  };
+  if (B > 1) {
+    if ((st = general(query, w_k, qt, Sq, Lat, D, D, Lat, 1, prec, (int64_t)Sq * D,
+                      (int64_t)Sq * Lat)) != MFA_SUCCESS)
+      return st;
+  }
+  // Q̃[b,h] (Sq x Lat) = Q[b,h] (Sq x D) · W_k[:, hD:(h+1)D]ᵀ, batched over h.
+  for (int b = 0; b < B && B == 1; ++b) {
+    mfa_gemm_descriptor_t g;
+    memset(&g, 0, sizeof(g));
+    g.M = Sq; g.N = Lat; g.K = D;
+    g.precision_a = g.precision_b = g.precision_c = prec;
+    g.transpose_b = 1;
+    g.lda = D; g.ldb = H * D; g.ldc = Lat;
+    g.batch = H;
+    g.stride_a = (uint64_t)Sq * D; g.stride_b = D; g.stride_c = (uint64_t)Sq * Lat;
+    const char* qa = (const char*)query + (int64_t)b * H * Sq * D * 2;
+    if ((st = mfa_gemm(&g, qa, w_k, qt + (int64_t)b * H * Sq * Lat * 2, stream)) != MFA_SUCCESS)
+      return st;
+  }
+  // Latent-space attention.
+  mfa::LatentParams lp;
+  memset(&lp, 0, sizeof(lp));
+  lp.q = qt; lp.lat = kv_latent; lp.olat = ot;
+  const Precisions pr = resolve_precisions(desc->base);
+  lp.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+  lp.l = logsumexp;
+  lp.B = B; lp.R = H * Sq; lp.Sq = Sq; lp.Skv = Skv;
+  lp.nblk = (lp.R + 31) / 32;
+  lp.c_log2 = 1.442695041f * resolve_scale(desc->base, D);
+  lp.causal = sp == MFA_SPARSITY_CAUSAL;
+  // Split the keys when the query blocks alone cannot fill the chip (decode shapes): aim at
+  // >= 512 workgroups, each split at least 4 tiles of 32 keys.
+  lp.nsplit = 1;
+  lp.chunk = Skv;
+  {
+    const int blocks = lp.nblk * B;
+    const int tiles = (Skv + 31) / 32;
+    int ns = (512 + blocks - 1) / blocks;
+    ns = std::min(ns, std::max(1, tiles / 4));
+    if (ns > 1) {
+      const int per = (tiles + ns - 1) / ns;   // tiles per split
+      lp.chunk = per * 32;
+      lp.nsplit = (tiles + per - 1) / per;
+    }
+  }
+  if (lp.nsplit > 1) {
+    const size_t obytes = (size_t)B * lp.nsplit * lp.R * Lat * 4;
+    const size_t mbytes = (size_t)B * lp.nsplit * lp.R * 8;
+    void* part = nullptr;
+    if ((st = scratch(obytes + mbytes, &part, 3)) != MFA_SUCCESS) return st;
+    lp.opart = (float*)part;
+    lp.mlpart = (float2*)((char*)part + obytes);
+  }
+  if ((st = hip_status(mfa::mla_latent_dispatch(lp, elem_of(prec), Lat, s),
+                       "MLA latent attention launch")) != MFA_SUCCESS)
+    return st;
+  // O[b,h] (Sq x D, FP32) = Õ[b,h] (Sq x Lat) · W_v[:, hD:(h+1)D], batched over h.
+  if (B > 1)
+    return general(ot, w_v, output, Sq, D, Lat, Lat, D, 0, MFA_PRECISION_FP32, (int64_t)Sq * Lat,
+                   (int64_t)Sq * D);
+  for (int b = 0; b < B; ++b) {
+    mfa_gemm_descriptor_t g;
+    memset(&g, 0, sizeof(g));
+    g.M = Sq; g.N = D; g.K = Lat;
+    g.precision_a = g.precision_b = prec;
+    g.precision_c = MFA_PRECISION_FP32;
+    g.lda = Lat; g.ldb = H * D; g.ldc = D;
+    g.batch = H;
+    g.stride_a = (uint64_t)Sq * Lat; g.stride_b = D; g.stride_c = (uint64_t)Sq * D;
+    if ((st = mfa_gemm(&g, ot + (int64_t)b * H * Sq * Lat * 2, w_v,
+                       output + (int64_t)b * H * Sq * D, stream)) != MFA_SUCCESS)
+      return st;
+  }
+  return MFA_SUCCESS;
+}

@@ -61,6 +61,8 @@ hipError_t fwd_wide_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 // INT8 K/V on the integer matrix cores (attention_fwd_i8.hip); 128-query blocks.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream);
+// MLA latent-space attention (attention_mla_latent.hip); lat = 256 or 512.
+hipError_t mla_latent_dispatch(const LatentParams& p, int elem, int lat, hipStream_t stream);
 // General GEMMDescriptor surface (gemm_general.hip); compute precision chosen from A and B.
 int gemm_general_compute(int prec_a, int prec_b);
 hipError_t gemm_general_dispatch(const GemmGParams& p, int batch, hipStream_t stream);

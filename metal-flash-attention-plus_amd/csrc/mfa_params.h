@@ -75,6 +75,23 @@ struct GemmParams {
   int32_t load_prev;
 };
 
+// MLA latent-space attention (attention_mla_latent.hip): query rows of every head of a batch
+// item flattened to [R = H·S_q][LAT]; the latent [S_kv][LAT] is both K and V.
+struct LatentParams {
+  const void* q;     // [B][R][LAT] 16-bit (Q·W_kᵀ)
+  const void* lat;   // [B][S_kv][LAT] 16-bit
+  void* olat;        // [B][R][LAT] 16-bit output (P·latent / l)
+  void* l;           // [B][R] L = m + log2 l (FP16 when l_f16), nullable
+  int32_t B, R, Sq, Skv, nblk;
+  float c_log2;      // softmax scale · log2(e)
+  int32_t causal, l_f16;
+  // Split-KV (decode shapes): nsplit workgroups per query block, `chunk` keys each, partial
+  // unnormalised Õ [B][nsplit][R][LAT] FP32 and (m, l) [B][nsplit][R] merged by a second pass.
+  int32_t nsplit, chunk;
+  float* opart;
+  float2* mlpart;
+};
+
 // General GEMM (gemm_general.hip): any FP32/FP16/BF16 mix, transposes, leading dimensions.
 struct GemmGParams {
   const void* a;
@@ -87,6 +104,7 @@ struct GemmGParams {
   int32_t esz_a, esz_b, esz_c;
   int32_t trans_a, trans_b;
   int32_t load_prev;
+  int32_t bmod;             // > 0: B's batch index is z % bmod (weights shared across an outer batch)
 };
 
 }  // namespace mfa

@@ -384,6 +384,9 @@ _sig("mfa_gemm", ctypes.c_int, [_P(GemmDescriptor), _V, _V, _V, _V])
 _sig("mfa_gemm_kernel_descriptor", ctypes.c_int, [_P(GemmDescriptor), _P(GemmKernelDescriptor)])
 _sig("mfa_mla_forward", ctypes.c_int,
      [_P(MLADescriptor), _V, _V, _V, _V, _V, _V, _V, _V, _V])
+_sig("mfa_mla_absorbed_workspace_size", ctypes.c_size_t, [_P(MLADescriptor)])
+_sig("mfa_mla_forward_absorbed", ctypes.c_int,
+     [_P(MLADescriptor), _V, _V, _V, _V, _V, _V, _V, _V])
 _sig("mfa_hadamard_rotate", ctypes.c_int, [_V, ctypes.c_uint32, ctypes.c_uint32, _V])
 _sig("mfa_hadamard_rotate_batch", ctypes.c_int, [_V, ctypes.c_uint32, _V])
 _sig("mfa_hadamard_scale", ctypes.c_float, [ctypes.c_uint32])
@@ -633,6 +636,21 @@ def mla_forward(base: AttentionDescriptor, kv_latent, w_k, w_v, query, output, B
     check(lib.mfa_mla_forward(ctypes.byref(d), _ptr(kv_latent), _ptr(w_k), _ptr(w_v), _ptr(query),
                               _ptr(k_buf), _ptr(v_buf), _ptr(output), _ptr(logsumexp),
                               _stream(stream)))
+
+
+def mla_forward_absorbed(base: AttentionDescriptor, kv_latent, w_k, w_v, query, output, B, H,
+                         S_q, S_kv, head_dim, latent_dim, precision: Precision, workspace=None,
+                         logsumexp=None, stream=None):
+    """Absorbed MLA (attention in the latent space; K/V never materialised)."""
+    d = MLADescriptor()
+    d.base = base
+    d.batch_size, d.num_heads = B, H
+    d.sequence_length_q, d.sequence_length_kv = S_q, S_kv
+    d.head_dim, d.kv_latent_dim = head_dim, latent_dim
+    d.precision = int(precision)
+    check(lib.mfa_mla_forward_absorbed(ctypes.byref(d), _ptr(kv_latent), _ptr(w_k), _ptr(w_v),
+                                       _ptr(query), _ptr(workspace), _ptr(output),
+                                       _ptr(logsumexp), _stream(stream)))
 
 
 def attention_flops(B, H, R, C, D, causal=False, kind="forward") -> float:

@@ -39,6 +39,21 @@ def main():
                                      transpose_b=tb))
         key = f"gemm_{pa.name}x{pb.name}_{'T' if ta else 'N'}{'T' if tb else 'N'}_{n}"
         out[key] = {"ms": round(ms, 4), "tflops": round(2 * n ** 3 / ms / 1e9, 1)}
+    # MLA: decompress path vs absorbed (latent-space) path, C4 prefill and a decode shape.
+    for (B, H, Sq, Skv) in [(1, 16, 4096, 4096), (32, 16, 1, 4096), (8, 16, 16, 8192)]:
+        D, lat = 128, 512
+        bf = torch.bfloat16
+        latent = torch.randn(B * Skv, lat, device="cuda").to(bf)
+        wk = (torch.randn(lat, H * D, device="cuda") * lat ** -0.5).to(bf)
+        wv = (torch.randn(lat, H * D, device="cuda") * lat ** -0.5).to(bf)
+        q = torch.randn(B, H, Sq, D, device="cuda").to(bf)
+        o = torch.empty(B, H, Sq, D, device="cuda")
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.BF16)
+        args = (base, latent, wk, wv, q, o, B, H, Sq, Skv, D, lat, P.BF16)
+        t_dec = timeit(lambda: mfa.mla_forward(*args))
+        t_abs = timeit(lambda: mfa.mla_forward_absorbed(*args))
+        out[f"mla_B{B}_H{H}_Sq{Sq}_Skv{Skv}"] = {"decompress_ms": round(t_dec, 4),
+                                                 "absorbed_ms": round(t_abs, 4)}
     nb, bs = 1 << 18, 1024
     x = torch.randn(nb, bs, device="cuda")
     hr = mfa.HadamardRotation()
