@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true")
     ap.add_argument("--no-mla", action="store_true")
+    ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8(f) rows")
     ap.add_argument("--c5-batch", type=int, default=8)
     return ap.parse_args()
 
@@ -213,6 +214,64 @@ def main():
             "ms_per_step": round(el4 / n4 * 1e3, 4),
         }
         del lat, wk, wv, q4, o4, kb4, vb4
+
+    # ------------------------------------------------- SURVEY §8(f) rows (one GPU's view)
+    if not args.no_next:
+        def ev_time(fn, steps):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / steps
+
+        nx = max(5, args.steps // 10)
+        nxt = {}
+        # Absorbed MLA at a decode shape: HBM-bound on the latent cache read.
+        Bd, Hd, Sqd, Skd, Dd, LATd = 32, 16, 1, 4096, 128, 512
+        latd = uniform((Bd * Skd, LATd), torch.bfloat16)
+        wkd = (uniform((LATd, Hd * Dd), torch.float32) * 0.176).to(torch.bfloat16)
+        wvd = (uniform((LATd, Hd * Dd), torch.float32) * 0.176).to(torch.bfloat16)
+        qd = uniform((Bd, Hd, Sqd, Dd), torch.bfloat16)
+        od = torch.empty((Bd, Hd, Sqd, Dd), dtype=torch.float32, device=dev)
+        based = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.BF16)
+        argsd = (based, latd, wkd, wvd, qd, od, Bd, Hd, Sqd, Skd, Dd, LATd, mfa.Precision.BF16)
+        ms_abs = ev_time(lambda: mfa.mla_forward_absorbed(*argsd, stream=stream), nx)
+        ms_dec = ev_time(lambda: mfa.mla_forward(*argsd, stream=stream), nx)
+        nxt["mla_absorbed_decode"] = {
+            "workload": "absorbed MLA, bf16, B32 H16 S_q 1 S_kv 4096, latent 512 -> D 128",
+            "ms": round(ms_abs, 4), "decompress_ms": round(ms_dec, 4),
+            "speedup_vs_decompress": round(ms_dec / ms_abs, 2),
+            "latent_GBps": round(Bd * Skd * LATd * 2 / ms_abs / 1e6, 1),
+        }
+        del latd, wkd, wvd, qd, od
+        # General GEMM (GEMMDescriptor surface): NN (tuned path) and NT / TN (general kernel).
+        ng = 4096
+        ga = uniform((ng, ng), torch.float16)
+        gb = uniform((ng, ng), torch.float16)
+        gc = torch.empty((ng, ng), dtype=torch.float32, device=dev)
+        for ta, tb in ((False, False), (False, True), (True, False)):
+            ms = ev_time(lambda: mfa.gemm(ga, gb, gc, ng, ng, ng, mfa.Precision.FP16,
+                                          mfa.Precision.FP32, transpose_a=ta, transpose_b=tb,
+                                          stream=stream), nx)
+            key = "gemm_fp16_" + ("T" if ta else "N") + ("T" if tb else "N") + "_4096"
+            nxt[key] = {"ms": round(ms, 4), "tflops": round(2 * ng ** 3 / ms / 1e9, 1),
+                        "roofline_frac": round(2 * ng ** 3 / ms / 1e9 / PEAK_FP16_TFLOPS, 4)}
+        del ga, gb, gc
+        # Hadamard rotation: 8 bytes per element against the 8 TB/s HBM roof.
+        hx = uniform((1 << 28,), torch.float32)
+        ms_h = ev_time(lambda: mfa.HadamardRotation().rotate(hx, 128, (1 << 28) // 128,
+                                                             stream=stream), nx)
+        gbs = 8 * (1 << 28) / ms_h / 1e6
+        nxt["hadamard_fp32_1GiB_block128"] = {"ms": round(ms_h, 4), "GBps": round(gbs, 1),
+                                              "roofline_frac": round(gbs / 8000.0, 4)}
+        del hx
+        result["next_rows"] = nxt
 
     # ---------------------------------------------------------------- headline: C2
     # Measured last: the sections above have brought the chip to its steady clock (a cold
