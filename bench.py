@@ -339,6 +339,8 @@ def main():
     # ---------------------------------------------------------------- CPU baseline
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(S, D, H)
+        if "next_rows" in result:
+            cpu_next_rows(result["next_rows"])
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -382,6 +384,50 @@ def cpu_baseline(S: int, D: int, H: int):
                       f"inputs), oracle/mfa_oracle.c forward, {dt:.2f} s wall on {threads} "
                       "threads; naive restatement of Network.swift (double accumulation; it "
                       "computes the masked columns too, as the reference's CPU oracle does)"}
+
+
+def cpu_next_rows(nxt: dict):
+    """The oracle's CPU rate beside each §8(f) row, on bounded samples (same threads as
+    cpu_baseline): GEMM 1024^3, Hadamard 64 MiB, absorbed-MLA decode on 4 of the 32 batch
+    items (oracle attention on the decompressed K/V: the reference's CPU path)."""
+    sys.path.insert(0, os.path.join(_REPO, "tests"))
+    import numpy as np
+    import oracle_lib as ol
+    threads = ol.set_threads(min(16, os.cpu_count() or 1))
+    rng = np.random.default_rng(1)
+    n = 1024
+    a, b = rng.random((n, n), dtype=np.float32), rng.random((n, n), dtype=np.float32)
+    t0 = time.perf_counter()
+    ol.gemm(a, b)
+    dt = time.perf_counter() - t0
+    cpu_gemm = {"tflops": round(2 * n ** 3 / dt / 1e12, 5), "cores": threads,
+                "sample": "oracle GEMM 1024^3 fp32 (double accumulation)"}
+    for k in nxt:
+        if k.startswith("gemm_"):
+            nxt[k]["cpu"] = cpu_gemm
+    x = rng.standard_normal(1 << 24).astype(np.float32)
+    t0 = time.perf_counter()
+    ol.hadamard(x, 128, float(np.float32(1 / np.sqrt(128.0))))
+    dt = time.perf_counter() - t0
+    if "hadamard_fp32_1GiB_block128" in nxt:
+        nxt["hadamard_fp32_1GiB_block128"]["cpu"] = {
+            "GBps": round(8 * x.size / dt / 1e9, 3), "cores": 1,
+            "sample": "oracle FWHT (the reference kernel's loops, one block after another), 64 MiB"}
+    if "mla_absorbed_decode" in nxt:
+        Bs, H, Skv, D, LAT = 4, 16, 4096, 128, 512
+        lat = rng.standard_normal((Bs * Skv, LAT)).astype(np.float32)
+        wk = (rng.standard_normal((LAT, H * D)) * LAT ** -0.5).astype(np.float32)
+        wv = (rng.standard_normal((LAT, H * D)) * LAT ** -0.5).astype(np.float32)
+        q = rng.standard_normal((Bs, H, 1, D)).astype(np.float32)
+        t0 = time.perf_counter()
+        K = ol.gemm(lat, wk).reshape(Bs, Skv, H, D).transpose(0, 2, 1, 3)
+        V = ol.gemm(lat, wv).reshape(Bs, Skv, H, D).transpose(0, 2, 1, 3)
+        ol.attention(np.ascontiguousarray(q), np.ascontiguousarray(K), np.ascontiguousarray(V))
+        dt = time.perf_counter() - t0
+        nxt["mla_absorbed_decode"]["cpu"] = {
+            "ms_full_workload": round(dt * 1e3 * 32 / Bs, 1), "cores": threads,
+            "sample": f"oracle decompress GEMMs + attention on {Bs} of the 32 batch items, "
+                      f"{dt:.2f} s, scaled x{32 // Bs}"}
 
 
 if __name__ == "__main__":
