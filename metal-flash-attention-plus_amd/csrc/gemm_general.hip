@@ -30,6 +30,7 @@
 #include "mfa_device.h"
 #include "mfa_params.h"
 #include "mfa_dispatch.h"
+#include <type_traits>
 
 namespace mfa {
 
@@ -50,7 +51,11 @@ __device__ __forceinline__ float load_elem(const char* base, int prec, int64_t i
 }  // namespace
 
 // CT: compute type — P_FP16 / P_BF16 (16-bit MFMA, A and B in that precision) or P_FP32.
-template <int CT>
+// LAY (16-bit only): bit 0 = A is m-contiguous (transposed), bit 1 = B is n-contiguous
+// (untransposed).  A 16-bit m/n-contiguous operand keeps its memory layout in LDS
+// ([32 k][128 m/n], Tile16<128>) and is read with ds_read_b64_tr_b16; the k-contiguous
+// operand is then read in the same permuted k order (two 8-byte reads), as gemm.hip does.
+template <int CT, int LAY = 0>
 __global__ void __launch_bounds__(256) mfa_gemm_general_kernel(GemmGParams p) {
   constexpr bool F32 = CT == P_FP32;
   constexpr int KT = F32 ? 16 : 32;                 // k per LDS tile
@@ -160,6 +165,12 @@ __global__ void __launch_bounds__(256) mfa_gemm_general_kernel(GemmGParams p) {
   auto store16 = [&](const Op& o, char* tile, int id, uint4 v) {
     int row, k;
     chunk_coords(o, id, 0, &row, &k);
+    if constexpr (LAY != 0) {
+      if (!o.kc) {  // memory layout kept: [k][128 m/n]
+        *reinterpret_cast<uint4*>(tile + Tile16<128>::off(k, row / 8)) = v;
+        return;
+      }
+    }
     if (o.kc) {
       *reinterpret_cast<uint4*>(tile + goff(row, k / 8)) = v;
     } else {
@@ -247,15 +258,28 @@ __global__ void __launch_bounds__(256) mfa_gemm_general_kernel(GemmGParams p) {
       }
     } else {
       using E = typename std::conditional<CT == P_FP16, F16, BF16>::type;
+      using AT = Arith16<E, 128>;
+      // k-contiguous operand read: standard k order, or the transposed reads' order.
+      auto kc_read = [&](const char* t, int r, int s) -> i16x8 {
+        if constexpr (LAY == 0) {
+          return *reinterpret_cast<const i16x8*>(t + goff(r, 2 * s + hh));
+        } else {
+          const uint2 lo = *reinterpret_cast<const uint2*>(t + goff(r, 2 * s) + 8 * hh);
+          const uint2 hi = *reinterpret_cast<const uint2*>(t + goff(r, 2 * s + 1) + 8 * hh);
+          return __builtin_bit_cast(i16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        }
+      };
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         i16x8 af[2], bf[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          af[i] = *reinterpret_cast<const i16x8*>(at + goff(wm * 64 + i * 32 + l32, 2 * s + hh));
+          af[i] = (LAY & 1) ? AT::read_tr(at, 0, s, wm * 64 + i * 32, lane)
+                            : kc_read(at, wm * 64 + i * 32 + l32, s);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          bf[j] = *reinterpret_cast<const i16x8*>(bt + goff(wn * 64 + j * 32 + l32, 2 * s + hh));
+          bf[j] = (LAY & 2) ? AT::read_tr(bt, 0, s, wn * 64 + j * 32, lane)
+                            : kc_read(bt, wn * 64 + j * 32 + l32, s);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -295,13 +319,21 @@ int gemm_general_compute(int prec_a, int prec_b) {
 
 hipError_t gemm_general_dispatch(const GemmGParams& p, int batch, hipStream_t stream) {
   const dim3 grid((p.N + GBN - 1) / GBN, (p.M + GBM - 1) / GBM, batch);
+  const int lay = (p.trans_a ? 1 : 0) | (p.trans_b ? 0 : 2);
+#define MFA_GG(CTV, L)                                                                      \
+  case L: {                                                                                 \
+    auto k = mfa_gemm_general_kernel<CTV, L>;                                               \
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, p);                                   \
+    break;                                                                                  \
+  }
   switch (gemm_general_compute(p.prec_a, p.prec_b)) {
     case P_FP16:
-      hipLaunchKernelGGL(mfa_gemm_general_kernel<P_FP16>, grid, dim3(256), 0, stream, p);
+      switch (lay) { MFA_GG(P_FP16, 0) MFA_GG(P_FP16, 1) MFA_GG(P_FP16, 2) MFA_GG(P_FP16, 3) }
       break;
     case P_BF16:
-      hipLaunchKernelGGL(mfa_gemm_general_kernel<P_BF16>, grid, dim3(256), 0, stream, p);
+      switch (lay) { MFA_GG(P_BF16, 0) MFA_GG(P_BF16, 1) MFA_GG(P_BF16, 2) MFA_GG(P_BF16, 3) }
       break;
+#undef MFA_GG
     default:
       hipLaunchKernelGGL(mfa_gemm_general_kernel<P_FP32>, grid, dim3(256), 0, stream, p);
       break;
@@ -309,8 +341,14 @@ hipError_t gemm_general_dispatch(const GemmGParams& p, int batch, hipStream_t st
   return hipGetLastError();
 }
 
-template __global__ void mfa_gemm_general_kernel<P_FP16>(GemmGParams);
-template __global__ void mfa_gemm_general_kernel<P_BF16>(GemmGParams);
+#define MFA_GG_INST(CTV)                                                   \
+  template __global__ void mfa_gemm_general_kernel<CTV, 0>(GemmGParams); \
+  template __global__ void mfa_gemm_general_kernel<CTV, 1>(GemmGParams); \
+  template __global__ void mfa_gemm_general_kernel<CTV, 2>(GemmGParams); \
+  template __global__ void mfa_gemm_general_kernel<CTV, 3>(GemmGParams);
+MFA_GG_INST(P_FP16)
+MFA_GG_INST(P_BF16)
+#undef MFA_GG_INST
 template __global__ void mfa_gemm_general_kernel<P_FP32>(GemmGParams);
 
 }  // namespace mfa
