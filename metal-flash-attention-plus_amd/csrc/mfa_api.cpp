@@ -1020,7 +1020,8 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
   char* ot = qt + qlat * 2;
   // One launch per GEMM over all (b, h): W_k / W_v slices depend on h only (bmod = H).
   auto general = [&](const void* a, const void* w, void* c, int M, int N, int K, int lda,
-                     int ldc, int trans_b, int prec_c, int64_t sa, int64_t sc) {
+                     int ldc, int trans_b, int prec_c, int64_t sa, int64_t sc, int nbatch,
+                     int bmod) {
     mfa::GemmGParams g;
     memset(&g, 0, sizeof(g));
     g.a = a; g.b = w; g.c = c;
@@ -1030,12 +1031,19 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
     g.prec_a = g.prec_b = prec; g.prec_c = prec_c;
     g.esz_a = g.esz_b = 2; g.esz_c = prec_c == MFA_PRECISION_FP32 ? 4 : 2;
     g.trans_b = trans_b;
-    g.bmod = H;
-    return hip_status(mfa::gemm_general_dispatch(g, B * H, s), "absorbed MLA GEMM launch");
+    g.bmod = bmod;
+    return hip_status(mfa::gemm_general_dispatch(g, nbatch, s), "absorbed MLA GEMM launch");
   };
-  if (B > 1) {
+  // Decode (S_q = 1): per head, the B query rows are one strided [B, D] matrix, so each head's
+  // weight slice is read once (M = B) instead of once per batch item.
+  const bool decode = Sq == 1 && B > 1;
+  if (decode) {
+    if ((st = general(query, w_k, qt, B, Lat, D, H * D, H * Lat, 1, prec, D, Lat, H, 0)) !=
+        MFA_SUCCESS)
+      return st;
+  } else if (B > 1) {
     if ((st = general(query, w_k, qt, Sq, Lat, D, D, Lat, 1, prec, (int64_t)Sq * D,
-                      (int64_t)Sq * Lat)) != MFA_SUCCESS)
+                      (int64_t)Sq * Lat, B * H, H)) != MFA_SUCCESS)
       return st;
   }
   // Q̃[b,h] (Sq x Lat) = Q[b,h] (Sq x D) · W_k[:, hD:(h+1)D]ᵀ, batched over h.
@@ -1090,9 +1098,12 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
                        "MLA latent attention launch")) != MFA_SUCCESS)
     return st;
   // O[b,h] (Sq x D, FP32) = Õ[b,h] (Sq x Lat) · W_v[:, hD:(h+1)D], batched over h.
+  if (decode)
+    return general(ot, w_v, output, B, D, Lat, H * Lat, H * D, 0, MFA_PRECISION_FP32, Lat, D, H,
+                   0);
   if (B > 1)
     return general(ot, w_v, output, Sq, D, Lat, Lat, D, 0, MFA_PRECISION_FP32, (int64_t)Sq * Lat,
-                   (int64_t)Sq * D);
+                   (int64_t)Sq * D, B * H, H);
   for (int b = 0; b < B; ++b) {
     mfa_gemm_descriptor_t g;
     memset(&g, 0, sizeof(g));
