@@ -337,7 +337,7 @@ def main():
     del q, k, v, o, l
 
     # ---------------------------------------------------------------- CPU baseline
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(S, D, H)
         if "next_rows" in result:
             cpu_next_rows(result["next_rows"])
