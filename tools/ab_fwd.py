@@ -56,6 +56,7 @@ def main():
     flop = 4 * D * (S * (S + 1) / 2 if causal else S * S) * B * H
     ref = None
     res = {x: [] for x in vals}
+    rel = {}
     for r in range(a.rounds):
         for x in vals:
             os.environ[var] = x
@@ -63,8 +64,10 @@ def main():
             torch.cuda.synchronize()
             if ref is None:
                 ref = o.clone()
+            elif i8:
+                rel[x] = float((o - ref).norm() / ref.norm())
             else:
-                assert torch.allclose(o, ref, atol=2e-3 if not i8 else 2e-2), f"{var}={x} differs"
+                assert torch.allclose(o, ref, atol=2e-3), f"{var}={x} differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
@@ -74,7 +77,7 @@ def main():
             res[x].append(e0.elapsed_time(e1) / a.reps)
     out = {x: {"ms_med": round(statistics.median(t), 4), "tflops": round(flop / statistics.median(t) / 1e9, 1)}
            for x, t in res.items()}
-    print(json.dumps({"cfg": a.cfg, "knob": var, **out}))
+    print(json.dumps({"cfg": a.cfg, "knob": var, **out, "relL2_vs_first": rel}))
 
 
 if __name__ == "__main__":
