@@ -112,3 +112,42 @@ def test_fast_backward_c5_slice_full_length(gpu):
     sum_dv = dv.double().sum(dim=2)
     sum_do = do.double().sum(dim=2)
     assert (sum_dv - sum_do).abs().max().item() <= 1e-2 * max(1.0, sum_do.abs().max().item())
+
+
+def test_c5_full_shard_slice_invariance(gpu):
+    # BASELINE configs[4] at its full per-GPU shard (B8 H32 S4096 D256 fp16, 256 slices):
+    # a size-independent property — every (batch, head) slice is independent, so the slices
+    # of the full launch must equal, bit for bit, the same slices run alone (whose numerics
+    # test_fast_backward_c5_slice_full_length pins).  Plus the dV column-sum identity on the
+    # whole shard.
+    B, H, S, D = 8, 32, 4096, 256
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(11)
+    q, k, v, do = ((torch.rand((B, H, S, D), generator=g, device=dev) - 0.5).half()
+                   for _ in range(4))
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=FP16)
+    mha = mfa.MultiHeadAttention()
+
+    def run(qq, kk, vv, dd):
+        b, h = qq.shape[0], qq.shape[1]
+        desc = mfa.MultiHeadDescriptor.make(base, b, h, S, D)
+        o = torch.empty((b, h, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((b, h, S), dtype=torch.float16, device=dev)
+        dq, dk, dv = (torch.empty((b, h, S, D), dtype=torch.float32, device=dev) for _ in range(3))
+        dbuf = torch.empty((b, h, S), dtype=torch.bfloat16, device=dev)
+        mha.forward(desc, qq, kk, vv, o, l)
+        mha.backward(desc, qq, kk, vv, o, dd, l, dq, dk, dv, dbuf)
+        torch.cuda.synchronize()
+        return o, l, dq, dk, dv
+
+    full = run(q, k, v, do)
+    for (bi, hi) in [(0, 0), (3, 17), (7, 31)]:
+        sl = lambda t: t[bi:bi + 1, hi:hi + 1].contiguous()
+        one = run(sl(q), sl(k), sl(v), sl(do))
+        for name, a, b1 in zip(("O", "L", "dQ", "dK", "dV"), full, one):
+            assert torch.equal(a[bi:bi + 1, hi:hi + 1], b1), f"{name} slice ({bi},{hi})"
+    dv = full[4]
+    sum_dv = dv.double().sum(dim=2)
+    sum_do = do.double().sum(dim=2)
+    assert (sum_dv - sum_do).abs().max().item() <= 1e-2 * max(1.0, sum_do.abs().max().item())
+    assert all(torch.isfinite(t).all() for t in full)
