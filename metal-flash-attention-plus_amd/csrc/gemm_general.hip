@@ -17,12 +17,12 @@
 //     FP32 register precision does for mixed inputs.
 //
 // Tiling: 128x128 outputs per workgroup of 4 waves (2x2, 64x64 per wave = 2x2 MFMA tiles).
-// Both operand tiles sit in LDS k-contiguous, [128 rows][64 bytes] (32 16-bit or 16 FP32
-// values of k per row), 16-byte chunks XOR-swizzled by (row >> 2) & 3.  An operand whose
-// memory layout is k-contiguous (A untransposed, B transposed) is staged with 16-byte
-// writes; one that is m/n-contiguous is read from HBM along m/n (coalesced) and written to
-// LDS transposed, element by element.  Register-staged double buffering: the next k-step's
-// chunks are loaded from HBM while the current one is multiplied.
+// A k-contiguous operand (A untransposed, B transposed) sits in LDS as [128 rows][64 bytes]
+// (32 16-bit or 16 FP32 values of k per row), 16-byte chunks XOR-swizzled by (row >> 2) & 3.
+// A 16-bit m/n-contiguous operand keeps its memory layout ([32 k][128], Tile16<128>) and is
+// read with the transposing LDS read (see the LAY parameter); an FP32 one is written to the
+// k-contiguous image element by element.  Register-staged double buffering: the next
+// k-step's chunks are loaded from HBM while the current one is multiplied.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -102,24 +102,22 @@ __global__ void __launch_bounds__(256) mfa_gemm_general_kernel(GemmGParams p) {
     chunk_coords(o, id, k0, &row, &k);
     const int gr = o.r0 + row;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    // The chunk's 8 elements are consecutive in memory along k (kc) or along m/n.
     const uint16_t* src;
     int nvalid;
-    int64_t step;
     if (o.kc) {
       if (gr >= o.rows) return v;
       src = (const uint16_t*)o.base + (int64_t)gr * o.ld + k;
       nvalid = p.K - k;
-      step = 1;
     } else {
       if (k >= p.K) return v;
       src = (const uint16_t*)o.base + (int64_t)k * o.ld + gr;
       nvalid = o.rows - gr;
-      step = 1;
     }
     if (nvalid >= 8 && (((uintptr_t)src) & 15) == 0) return *reinterpret_cast<const uint4*>(src);
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     for (int j = 0; j < 8; ++j)
-      if (j < nvalid) w[j >> 1] |= (uint32_t)src[j * step] << (16 * (j & 1));
+      if (j < nvalid) w[j >> 1] |= (uint32_t)src[j] << (16 * (j & 1));
     return make_uint4(w[0], w[1], w[2], w[3]);
   };
   auto loadf = [&](const Op& o, int id, int k0, float (&v)[8]) {
