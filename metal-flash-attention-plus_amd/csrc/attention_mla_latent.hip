@@ -37,11 +37,12 @@ __global__ void __launch_bounds__(256, 2) mfa_mla_latent_kernel(LatentParams p) 
   constexpr int CPR = LAT / 8;             // 16-byte chunks per latent row
   constexpr int CPT = BK * CPR / NT;       // chunks staged per thread
   constexpr int TILEB = BK * LAT * 2;
+  constexpr int XST = 16;                  // floats per lane in the exchange area
   using A = Arith16<E, LAT>;
   using TT = Tile16<LAT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const tb0 = smem;                              // 2 latent tiles
-  float* const xb = reinterpret_cast<float*>(smem + 2 * TILEB);  // [4 waves][16][64]
+  float* const xb = reinterpret_cast<float*>(smem + 2 * TILEB);  // [4 waves][64 lanes][XST]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -117,14 +118,32 @@ __global__ void __launch_bounds__(256, 2) mfa_mla_latent_kernel(LatentParams p) 
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds)
       sp = A::mma(A::read_row(kt, l32, wave * DS + ds, hh), qf[ds], sp);
+    // Exchange: each lane's 16 partial values contiguous ([wave][lane][16 floats]); the four
+    // 16-byte chunks are rotated by (lane >> 2) & 3 so the lanes of a ds_read_b128 group hit
+    // distinct banks.
+    const int xsw = (lane >> 2) & 3;
+    {
+      float* dst = xb + (wave * 64 + lane) * XST;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) xb[(wave * 16 + i) * 64 + lane] = sp[i];
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(dst + 4 * (q ^ xsw)) =
+            f32x4{sp[4 * q], sp[4 * q + 1], sp[4 * q + 2], sp[4 * q + 3]};
+    }
     __syncthreads();
     f32x16 s;
+    {
+      f32x4 part[4][4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      s[i] = ((xb[i * 64 + lane] + xb[(16 + i) * 64 + lane]) + xb[(32 + i) * 64 + lane]) +
-             xb[(48 + i) * 64 + lane];
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          part[w][q] = *reinterpret_cast<const f32x4*>(xb + (w * 64 + lane) * XST + 4 * (q ^ xsw));
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          s[4 * q + e] = ((part[0][q][e] + part[1][q][e]) + part[2][q][e]) + part[3][q][e];
+    }
 
     if (t + BK > p.Skv || (p.causal && t + BK - 1 > spos)) {
       MFA_KEEP_BRANCH();
@@ -258,7 +277,7 @@ __global__ void __launch_bounds__(LAT / 4) mfa_mla_latent_merge_kernel(LatentPar
 
 template <class E, int LAT>
 static hipError_t launch_latent(const LatentParams& p, hipStream_t stream) {
-  constexpr int LDS = 2 * 32 * LAT * 2 + 4 * 16 * 64 * 4;
+  constexpr int LDS = 2 * 32 * LAT * 2 + 4 * 64 * 16 * 4;
   auto kern = mfa_mla_latent_kernel<E, LAT>;
   static bool attr_set = false;
   if (!attr_set) {
