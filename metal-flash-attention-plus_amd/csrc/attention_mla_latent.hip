@@ -260,12 +260,32 @@ __global__ void __launch_bounds__(LAT / 4) mfa_mla_latent_merge_kernel(LatentPar
   l += kFltMin;
   if (!(l > 0.f)) l = kFltMin;
   const float inv = 1.f / l;
-  ushort4 v;
-  v.x = E::from_f32(acc.x * inv);
-  v.y = E::from_f32(acc.y * inv);
-  v.z = E::from_f32(acc.z * inv);
-  v.w = E::from_f32(acc.w * inv);
-  *reinterpret_cast<ushort4*>((uint16_t*)p.olat + row * LAT + d) = v;
+  if (p.wv) {
+    // Fused output projection: Õ row (FP32) through LDS, then one output dim per thread.
+    __shared__ float orow[LAT];
+    *reinterpret_cast<float4*>(orow + d) =
+        make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    __syncthreads();
+    const int hq = r / p.Sq;
+    const uint16_t* w = (const uint16_t*)p.wv + (int64_t)hq * p.D;
+    const int64_t ldw = (int64_t)p.H * p.D;
+    for (int dd = threadIdx.x; dd < p.D; dd += LAT / 4) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < LAT; k += 2) {
+        a0 = __builtin_fmaf(orow[k], E::to_f32(w[(int64_t)k * ldw + dd]), a0);
+        a1 = __builtin_fmaf(orow[k + 1], E::to_f32(w[(int64_t)(k + 1) * ldw + dd]), a1);
+      }
+      p.out[row * p.D + dd] = a0 + a1;
+    }
+  } else {
+    ushort4 v;
+    v.x = E::from_f32(acc.x * inv);
+    v.y = E::from_f32(acc.y * inv);
+    v.z = E::from_f32(acc.z * inv);
+    v.w = E::from_f32(acc.w * inv);
+    *reinterpret_cast<ushort4*>((uint16_t*)p.olat + row * LAT + d) = v;
+  }
   if (threadIdx.x == 0 && p.l) {
     const float L = M + __log2f(l);
     if (p.l_f16)

@@ -1093,10 +1093,16 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
     if ((st = scratch(obytes + mbytes, &part, 3)) != MFA_SUCCESS) return st;
     lp.opart = (float*)part;
     lp.mlpart = (float2*)((char*)part + obytes);
+    // The merge pass applies W_v itself (FP32 Õ, one launch fewer).
+    lp.wv = w_v;
+    lp.out = output;
+    lp.H = H;
+    lp.D = D;
   }
   if ((st = hip_status(mfa::mla_latent_dispatch(lp, elem_of(prec), Lat, s),
                        "MLA latent attention launch")) != MFA_SUCCESS)
     return st;
+  if (lp.wv) return MFA_SUCCESS;
   // O[b,h] (Sq x D, FP32) = Õ[b,h] (Sq x Lat) · W_v[:, hD:(h+1)D], batched over h.
   if (decode)
     return general(ot, w_v, output, B, D, Lat, H * Lat, H * D, 0, MFA_PRECISION_FP32, Lat, D, H,

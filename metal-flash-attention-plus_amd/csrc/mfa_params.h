@@ -90,6 +90,11 @@ struct LatentParams {
   int32_t nsplit, chunk;
   float* opart;
   float2* mlpart;
+  // Split path only: the merge also applies W_v (O[b,h,s,:] = Õ·W_v[:, h·D:(h+1)·D], FP32
+  // output) when wv != nullptr, so no separate output GEMM runs.
+  const void* wv;    // [LAT][H·D] 16-bit
+  float* out;        // [B][H][S_q][D]
+  int32_t H, D;
 };
 
 // General GEMM (gemm_general.hip): any FP32/FP16/BF16 mix, transposes, leading dimensions.
