@@ -232,6 +232,14 @@ __device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p
   }
 }
 
+__device__ __forceinline__ void store_l(const FwdParams& p, float L, int b, int h, int qi) {
+  const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
+  if (p.l_f16)
+    reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+  else
+    reinterpret_cast<float*>(p.l)[li] = L;
+}
+
 template <int DP>
 __device__ __forceinline__ void store_o_l(const FwdParams& p, const f32x16 (&o)[DP / 32],
                                           float m, float l, int b, int h, int qi, int hh) {
@@ -455,6 +463,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
       mml[(wg * 2 + 1) * 64 + lane] = st.lh;
     }
     __syncthreads();
+    float inv = 0.f;
     if (g == 0) {
       const float mb = mml[(wg * 2 + 0) * 64 + lane];
       const float lb = mml[(wg * 2 + 1) * 64 + lane];
@@ -468,7 +477,37 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           st.o[dt][i] = st.o[dt][i] * ca + mrg[((wg * ND + dt) * 16 + i) * 64 + lane] * cb;
-      if (qvalid) store_o_l<DP>(p, st.o, mf, l, b, h, qi, hh);
+      inv = p.o_mul / l;
+      if (hh == 0 && qvalid) store_l(p, mf + __log2f(l), b, h, qi);
+    }
+    __syncthreads();
+    // O leaves through LDS as whole rows (T21): group 0 writes its lanes' rows into a padded
+    // [BQ][DP] fp32 image over the (now free) merge area, then all 2·NT threads store 16-byte
+    // chunks along the rows, one wave instruction covering 1 KiB of consecutive O bytes
+    // instead of 64 rows x 16 B.
+    constexpr int ORS = DP * 4 + 16;  // padded row stride (bytes): conflict-free b128 writes
+    if (g == 0) {
+      char* orow = smem + (wg * 32 + l32) * ORS;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          *reinterpret_cast<float4*>(orow + (dt * 32 + 8 * gq + 4 * hh) * 4) =
+              make_float4(st.o[dt][4 * gq] * inv, st.o[dt][4 * gq + 1] * inv,
+                          st.o[dt][4 * gq + 2] * inv, st.o[dt][4 * gq + 3] * inv);
+    }
+    __syncthreads();
+    {
+      constexpr int CPR = DP / 4;  // 16-byte chunks per row
+      float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+#pragma unroll
+      for (int k = 0; k < BQ * CPR / (2 * NT); ++k) {
+        const int idx = k * 2 * NT + tid;
+        const int r = idx / CPR, d = (idx % CPR) * 4;
+        if (q0 + r < p.R && d < p.D)
+          *reinterpret_cast<float4*>(obase + (int64_t)(q0 + r) * p.o_ss + d) =
+              *reinterpret_cast<const float4*>(smem + r * ORS + d * 4);
+      }
     }
     __syncthreads();
     MFA_STAMP(3 + 3 * which);
@@ -496,6 +535,7 @@ template <class E, int DP, int BK, int NWG>
 static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 8 * BK * DP * 2;
   static_assert(LDS >= NWG * (DP / 32) * 16 * 64 * 4 + NWG * 2 * 64 * 4, "merge area");
+  static_assert(LDS >= NWG * 32 * (DP * 4 + 16), "O row image");
   auto kern = mfa_fwd2_pair_kernel<E, DP, BK, NWG>;
   static bool attr_set = false;
   if (!attr_set) {
