@@ -239,59 +239,142 @@ __global__ void __launch_bounds__(256, 2) mfa_mla_latent_kernel(LatentParams p) 
 
 // Merge of the key splits (flash-decoding): M = max m_s, w_s = exp2(m_s − M),
 // Õ = Σ w_s Õ_s / Σ w_s l_s, L = M + log2 Σ w_s l_s.  One workgroup of LAT/4 threads per row.
-template <class E, int LAT>
-__global__ void __launch_bounds__(LAT / 4) mfa_mla_latent_merge_kernel(LatentParams p) {
-  const int64_t row = blockIdx.x;             // b·R + r
-  const int b = (int)(row / p.R), r = (int)(row % p.R);
-  const int d = 4 * threadIdx.x;
-  float M = -kFltMax;
-  for (int s = 0; s < p.nsplit; ++s)
-    M = fmaxf(M, p.mlpart[((int64_t)b * p.nsplit + s) * p.R + r].x);
-  float l = 0.f;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = 0; s < p.nsplit; ++s) {
-    const int64_t prow = ((int64_t)b * p.nsplit + s) * p.R + r;
-    const float2 ml = p.mlpart[prow];
-    const float w = __builtin_amdgcn_exp2f(ml.x - M);
-    l += w * ml.y;
-    const float4 x = *reinterpret_cast<const float4*>(p.opart + prow * LAT + d);
-    acc.x += w * x.x; acc.y += w * x.y; acc.z += w * x.z; acc.w += w * x.w;
-  }
-  l += kFltMin;
-  if (!(l > 0.f)) l = kFltMin;
-  const float inv = 1.f / l;
-  if (p.wv) {
-    // Fused output projection: Õ row (FP32) through LDS, then one output dim per thread.
-    __shared__ float orow[LAT];
-    *reinterpret_cast<float4*>(orow + d) =
-        make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
-    __syncthreads();
-    const int hq = r / p.Sq;
-    const uint16_t* w = (const uint16_t*)p.wv + (int64_t)hq * p.D;
-    const int64_t ldw = (int64_t)p.H * p.D;
-    for (int dd = threadIdx.x; dd < p.D; dd += LAT / 4) {
-      float a0 = 0.f, a1 = 0.f;
-#pragma unroll 8
-      for (int k = 0; k < LAT; k += 2) {
-        a0 = __builtin_fmaf(orow[k], E::to_f32(w[(int64_t)k * ldw + dd]), a0);
-        a1 = __builtin_fmaf(orow[k + 1], E::to_f32(w[(int64_t)(k + 1) * ldw + dd]), a1);
+// Merge pass: MNB rows (the same query row r of MNB consecutive batch items) per 256-thread
+// workgroup (launched with MNB = 1).  The split states are combined per row into an FP32 Õ row image in LDS; with W_v,
+// the projection then reads each W_v element once for all MNB rows (the W_v columns of one
+// head are shared by every batch item), with the latent dimension split over two thread halves.
+constexpr int MNT = 256;
+
+template <class E, int LAT, int MNB>
+__global__ void __launch_bounds__(MNT) mfa_mla_latent_merge_kernel(LatentParams p) {
+  constexpr int TPR = LAT / 4;        // threads per row in the combine step (4 dims each)
+  constexpr int RPI = MNT / TPR;      // rows combined per iteration
+  // Õ rows [MNB][LAT], then (projection) 16 k groups' partial sums [16][MNB][128].
+  __shared__ __attribute__((aligned(16))) float smf[MNB * LAT + 16 * MNB * 128];
+  float (*orow)[LAT] = reinterpret_cast<float (*)[LAT]>(smf);
+  const int r = blockIdx.x % p.R;
+  const int b0 = (blockIdx.x / p.R) * MNB;
+  const int tid = threadIdx.x;
+  const int d = 4 * (tid % TPR);
+  for (int nb = tid / TPR; nb < MNB; nb += RPI) {
+    const int b = b0 + nb;
+    if (b >= p.B) break;
+    // SU splits' loads in flight at a time (a one-split-at-a-time loop is a chain of HBM
+    // latencies), merged online: running max M, rescaled sum l and Õ accumulator.
+    constexpr int SU = 16;
+    float M = -kFltMax;
+    float l = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s0 = 0; s0 < p.nsplit; s0 += SU) {
+      float2 ml[SU];
+      float4 x[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        ml[u] = make_float2(-kFltMax, 0.f);
+        x[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s0 + u < p.nsplit) {
+          const int64_t prow = ((int64_t)b * p.nsplit + s0 + u) * p.R + r;
+          ml[u] = p.mlpart[prow];
+          x[u] = *reinterpret_cast<const float4*>(p.opart + prow * LAT + d);
+        }
       }
-      p.out[row * p.D + dd] = a0 + a1;
+      float Mc = M;
+#pragma unroll
+      for (int u = 0; u < SU; ++u) Mc = fmaxf(Mc, ml[u].x);
+      const float cr = __builtin_amdgcn_exp2f(M - Mc);
+      M = Mc;
+      l *= cr;
+      acc.x *= cr; acc.y *= cr; acc.z *= cr; acc.w *= cr;
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const float w = __builtin_amdgcn_exp2f(ml[u].x - M);
+        l += w * ml[u].y;
+        acc.x += w * x[u].x; acc.y += w * x[u].y; acc.z += w * x[u].z; acc.w += w * x[u].w;
+      }
     }
-  } else {
-    ushort4 v;
-    v.x = E::from_f32(acc.x * inv);
-    v.y = E::from_f32(acc.y * inv);
-    v.z = E::from_f32(acc.z * inv);
-    v.w = E::from_f32(acc.w * inv);
-    *reinterpret_cast<ushort4*>((uint16_t*)p.olat + row * LAT + d) = v;
+    l += kFltMin;
+    if (!(l > 0.f)) l = kFltMin;
+    const float inv = 1.f / l;
+    const int64_t row = (int64_t)b * p.R + r;
+    if (p.wv) {
+      *reinterpret_cast<float4*>(&orow[nb][d]) =
+          make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    } else {
+      ushort4 v;
+      v.x = E::from_f32(acc.x * inv);
+      v.y = E::from_f32(acc.y * inv);
+      v.z = E::from_f32(acc.z * inv);
+      v.w = E::from_f32(acc.w * inv);
+      *reinterpret_cast<ushort4*>((uint16_t*)p.olat + row * LAT + d) = v;
+    }
+    if (d == 0 && p.l) {
+      const float L = M + __log2f(l);
+      if (p.l_f16)
+        reinterpret_cast<uint16_t*>(p.l)[row] = f32_to_f16(L);
+      else
+        reinterpret_cast<float*>(p.l)[row] = L;
+    }
   }
-  if (threadIdx.x == 0 && p.l) {
-    const float L = M + __log2f(l);
-    if (p.l_f16)
-      reinterpret_cast<uint16_t*>(p.l)[row] = f32_to_f16(L);
-    else
-      reinterpret_cast<float*>(p.l)[row] = L;
+  if (!p.wv) return;
+  __syncthreads();
+  // Fused output projection O[b, r, :] = Õ[b, r, :]·W_v[:, h·D : (h+1)·D], per 128-dim chunk:
+  // lane group dg (16 lanes) x k group kg (16 per workgroup) — each thread loads 8 consecutive
+  // W_v dims (16 B) for LAT/16 latent rows, all loads independent, and keeps 8 x MNB partial
+  // sums; the 16 k groups are summed through LDS.
+  const int nbv = min(MNB, p.B - b0);
+  const int hq = r / p.Sq;
+  const uint16_t* w = (const uint16_t*)p.wv + (int64_t)hq * p.D;
+  const int64_t ldw = (int64_t)p.H * p.D;
+  const bool vec = (p.D % 8) == 0 && (ldw % 8) == 0 && ((uintptr_t)p.wv % 16) == 0;
+  const int dg = tid & 15, kg = tid >> 4;
+  constexpr int KPG = LAT / 16;
+  float* red = smf + MNB * LAT;  // [16 k groups][MNB][128]
+  for (int dd0 = 0; dd0 < p.D; dd0 += 128) {
+    float acc[MNB][8];
+#pragma unroll
+    for (int nb = 0; nb < MNB; ++nb)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[nb][j] = 0.f;
+    const int dd = dd0 + 8 * dg;
+    if (dd < p.D) {
+#pragma unroll 16
+      for (int kk = 0; kk < KPG; ++kk) {
+        const int k = kg * KPG + kk;
+        const uint16_t* wr = w + (int64_t)k * ldw + dd;
+        float wf[8];
+        if (vec) {
+          const i16x8 w8 = *reinterpret_cast<const i16x8*>(wr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wf[j] = E::to_f32((uint16_t)w8[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wf[j] = dd + j < p.D ? E::to_f32(wr[j]) : 0.f;
+        }
+#pragma unroll
+        for (int nb = 0; nb < MNB; ++nb) {
+          const float o = orow[nb][k];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[nb][j] = __builtin_fmaf(o, wf[j], acc[nb][j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < MNB; ++nb)
+#pragma unroll
+      for (int j = 0; j < 8; j += 4)
+        *reinterpret_cast<float4*>(red + (kg * MNB + nb) * 128 + 8 * dg + j) =
+            make_float4(acc[nb][j], acc[nb][j + 1], acc[nb][j + 2], acc[nb][j + 3]);
+    __syncthreads();
+    for (int o = tid; o < MNB * 128; o += MNT) {
+      const int nb = o >> 7, dl = o & 127;
+      if (nb < nbv && dd0 + dl < p.D) {
+        float sum = 0.f;
+#pragma unroll
+        for (int g2 = 0; g2 < 16; ++g2) sum += red[(g2 * MNB + nb) * 128 + dl];
+        p.out[((int64_t)(b0 + nb) * p.R + r) * p.D + dd0 + dl] = sum;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -308,8 +391,10 @@ static hipError_t launch_latent(const LatentParams& p, hipStream_t stream) {
   }
   hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.nsplit), dim3(256), LDS, stream, p);
   if (p.nsplit > 1) {
-    auto merge = mfa_mla_latent_merge_kernel<E, LAT>;
-    hipLaunchKernelGGL(merge, dim3(p.B * p.R), dim3(LAT / 4), 0, stream, p);
+    // One row per workgroup measured fastest (B32 S_q 1: MNB 1/2/4 = 14.5/15.6/17.9 us): the
+    // W_v re-reads per batch item come from L2.
+    hipLaunchKernelGGL((mfa_mla_latent_merge_kernel<E, LAT, 1>), dim3(p.B * p.R), dim3(MNT), 0,
+                       stream, p);
   }
   return hipGetLastError();
 }
@@ -323,10 +408,10 @@ hipError_t mla_latent_dispatch(const LatentParams& p, int elem, int lat, hipStre
 }
 
 template __global__ void mfa_mla_latent_kernel<F16, 512>(LatentParams);
-template __global__ void mfa_mla_latent_merge_kernel<F16, 512>(LatentParams);
-template __global__ void mfa_mla_latent_merge_kernel<BF16, 512>(LatentParams);
-template __global__ void mfa_mla_latent_merge_kernel<F16, 256>(LatentParams);
-template __global__ void mfa_mla_latent_merge_kernel<BF16, 256>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<F16, 512, 1>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<BF16, 512, 1>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<F16, 256, 1>(LatentParams);
+template __global__ void mfa_mla_latent_merge_kernel<BF16, 256, 1>(LatentParams);
 template __global__ void mfa_mla_latent_kernel<BF16, 512>(LatentParams);
 template __global__ void mfa_mla_latent_kernel<F16, 256>(LatentParams);
 template __global__ void mfa_mla_latent_kernel<BF16, 256>(LatentParams);

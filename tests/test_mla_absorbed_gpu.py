@@ -78,6 +78,19 @@ def test_absorbed_decode_shapes(gpu, Sq, Skv):
     assert relerr(oa, od) < 2e-2
 
 
+@pytest.mark.parametrize("B,D", [(6, 64), (5, 192), (9, 128)])
+def test_absorbed_decode_batch_groups(gpu, B, D):
+    # The split-KV merge combines 4 batch items per workgroup and projects through W_v in
+    # 128-dim chunks: batch counts that are not multiples of 4, and D > 128.
+    H, Sq, Skv, latent, prec = 4, 1, 1500, 512, P.BF16
+    ((oa, _), (od, _)), (lat, wk, wv, Q) = run_both(B, H, Sq, Skv, D, latent, prec, False, seed=B)
+    K = bhsd(ol.gemm(lat, wk), B, Skv, H, D)
+    V = bhsd(ol.gemm(lat, wv), B, Skv, H, D)
+    ref = ol.attention(Q, K, V)
+    assert maxerr(oa, ref["O"]) < 1e-1
+    assert relerr(oa, od) < 2e-2
+
+
 def test_absorbed_config4(gpu):
     # BASELINE.json configs[3] shape (H16 assumed): both GPU paths agree; one head
     # against the oracle on the exact decompressed K/V.

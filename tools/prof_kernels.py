@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Runs one hot-path configuration a few times (a short program for rocprofv3 PMC passes).
-Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv} [reps]"""
+Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv,mla_dec} [reps]"""
 import os
 import sys
 
@@ -25,6 +25,17 @@ if which in ("c2", "c3"):
     desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
     for _ in range(reps):
         mha.forward(desc, q, k, v, o, l)
+elif which == "mla_dec":
+    # Absorbed MLA decode, as bench.py's next_rows entry (B32 H16 S_q 1 S_kv 4096, latent 512).
+    B, H, Sq, Skv, D, LAT = 32, 16, 1, 4096, 128, 512
+    lat = u((B * Skv, LAT), torch.bfloat16)
+    wk = (u((LAT, H * D), torch.float32) * 0.7).to(torch.bfloat16)
+    wv = (u((LAT, H * D), torch.float32) * 0.7).to(torch.bfloat16)
+    q = u((B, H, Sq, D), torch.bfloat16)
+    o = torch.empty((B, H, Sq, D), dtype=torch.float32, device=dev)
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.BF16)
+    for _ in range(reps):
+        mfa.mla_forward_absorbed(base, lat, wk, wv, q, o, B, H, Sq, Skv, D, LAT, mfa.Precision.BF16)
 elif which == "c3i8":
     B, H, S, D = 1, 16, 8192, 128
     qf = u((B, H, S, D), torch.float16)
