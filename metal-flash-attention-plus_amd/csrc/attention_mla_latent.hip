@@ -238,11 +238,10 @@ __global__ void __launch_bounds__(256, 2) mfa_mla_latent_kernel(LatentParams p) 
 }
 
 // Merge of the key splits (flash-decoding): M = max m_s, w_s = exp2(m_s − M),
-// Õ = Σ w_s Õ_s / Σ w_s l_s, L = M + log2 Σ w_s l_s.  One workgroup of LAT/4 threads per row.
-// Merge pass: MNB rows (the same query row r of MNB consecutive batch items) per 256-thread
-// workgroup (launched with MNB = 1).  The split states are combined per row into an FP32 Õ row image in LDS; with W_v,
-// the projection then reads each W_v element once for all MNB rows (the W_v columns of one
-// head are shared by every batch item), with the latent dimension split over two thread halves.
+// Õ = Σ w_s Õ_s / Σ w_s l_s, L = M + log2 Σ w_s l_s.  MNB rows (the same query row r of MNB
+// consecutive batch items) per 256-thread workgroup, launched with MNB = 1.  The split states
+// are combined per row into an FP32 Õ row image in LDS; with W_v, the projection then reads
+// each W_v element once for the workgroup's rows, the latent dimension split over 16 k groups.
 constexpr int MNT = 256;
 
 template <class E, int LAT, int MNB>
