@@ -249,11 +249,6 @@ hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, 
     if (e != hipErrorNotSupported) return e;
   }
   if (fast_eligible(p, elem, DP, kvsrc)) {
-    const char* var = getenv("MFA_FWD_VARIANT");
-    if (kvsrc == 0 && DP == 128 && var && var[0] == 'w') {
-      hipError_t e = mfa::fwd_wide_dispatch(p, elem, s);
-      if (e != hipErrorNotSupported) return e;
-    }
     hipError_t e = mfa::fwd_fast_dispatch(p, elem, DP, kvsrc, s);
     if (e != hipErrorNotSupported) return e;
   }

@@ -56,8 +56,6 @@ hipError_t bwd_fast_dispatch(const BwdParams& p, int kind, int elem, int DP, hip
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 hipError_t fwd_fast_dispatch(const FwdParams& p, int elem, int DP, int kvsrc, hipStream_t stream);
-// One-wave-per-SIMD forward with two query blocks per wave (attention_fwd_wide.hip).
-hipError_t fwd_wide_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 // INT8 K/V on the integer matrix cores (attention_fwd_i8.hip); 128-query blocks.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream);
