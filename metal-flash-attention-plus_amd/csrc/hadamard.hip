@@ -5,10 +5,10 @@
 // The reference runs one thread per block, stage by stage: at stage s every pair
 // (i, i + 2^s) becomes (a + b, a − b) (:118-129).  Every output element of a stage depends
 // only on the stage's two inputs, so any schedule that keeps the stage order gives the same
-// bits.  Here each lane holds R = min(block, 16) consecutive elements (four 16-byte loads), a
-// block spans block/R lanes of one wave, stages with stride < R run in registers and the
-// rest exchange whole registers with the lane `stride / R` away (ds_swizzle-free
-// __shfl_xor).  The lower element of a pair computes mine + other, the upper other − mine:
+// bits.  Blocks of 4 or more elements use mfa_hadamard_wave_kernel (coalesced wave layout,
+// below); blocks of 1 or 2 use mfa_hadamard_kernel, where each lane holds R = block
+// consecutive elements (with R = 16, stages with stride < R run in registers and the rest
+// exchange whole registers with the lane `stride / R` away).  The lower element of a pair computes mine + other, the upper other − mine:
 // the reference's a + b and a − b operand for operand.
 //
 // Scale: the reference multiplies by Metal's rsqrt((float)N) (:132-135).  Here it is the
@@ -80,11 +80,92 @@ __global__ void __launch_bounds__(256) mfa_hadamard_kernel(float* __restrict__ d
   }
 }
 
+// Blocks of N >= 4: each wave owns 256·I consecutive elements (I = max(1, N/256)) and reads
+// them with I fully coalesced 16-byte-per-lane instructions (instruction i, lane l: elements
+// 256·i + 4·l .. +3), so lane l holds v[4i + k] = element 256·i + 4·l + k.  The element-index
+// bits are then k (strides 1, 2: in registers), lane (strides 4 .. 128: __shfl_xor by
+// stride / 4) and i (strides 256, 512: in registers), and the stages still run in increasing
+// stride order with the reference's operands (lower: a + b, upper: a − b).  (Measured on a
+// 1 GiB buffer: 5.6-6.0 TB/s vs 5.0-5.1 for 16 consecutive elements per lane.)
+template <int I>
+__global__ void __launch_bounds__(256) mfa_hadamard_wave_kernel(float* __restrict__ data,
+                                                                int log2n, uint64_t total,
+                                                                float scale) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wbase = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (256 * I);
+  const int n = 1 << log2n;
+  float v[4 * I];
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    const uint64_t e = wbase + 256 * i + 4 * lane;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) x = *reinterpret_cast<const float4*>(data + e);
+    v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+  }
+  // Strides 1 and 2 (k bits).
+#pragma unroll
+  for (int st = 1; st <= 2; st <<= 1) {
+    if (st >= n) break;
+#pragma unroll
+    for (int j = 0; j < 4 * I; ++j) {
+      if (j & st) continue;
+      const float a = v[j], b = v[j + st];
+      v[j] = a + b;
+      v[j + st] = a - b;
+    }
+  }
+  // Strides 4 .. 128 (lane bits).
+  for (int d = 1; d <= 32 && 4 * d < n; d <<= 1) {
+    const bool upper = (lane & d) != 0;
+#pragma unroll
+    for (int j = 0; j < 4 * I; ++j) {
+      const float o = __shfl_xor(v[j], d);
+      v[j] = upper ? o - v[j] : v[j] + o;
+    }
+  }
+  // Strides 256 and 512 (i bits: register groups of 4).
+#pragma unroll
+  for (int e = 1; e < I; e <<= 1) {
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      if (i & e) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float a = v[4 * i + k], b = v[4 * (i + e) + k];
+        v[4 * i + k] = a + b;
+        v[4 * (i + e) + k] = a - b;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    const uint64_t e = wbase + 256 * i + 4 * lane;
+    if (e < total)
+      *reinterpret_cast<float4*>(data + e) = make_float4(v[4 * i] * scale, v[4 * i + 1] * scale,
+                                                         v[4 * i + 2] * scale, v[4 * i + 3] * scale);
+  }
+}
+
 hipError_t hadamard_dispatch(float* data, int log2n, uint64_t num_blocks, float scale,
                              hipStream_t stream) {
   const uint64_t n = 1ull << log2n;
   const uint64_t total = n * num_blocks;
-  const int R = n >= 16 ? 16 : (int)n;
+  if (n >= 4) {
+    const int I = n >= 1024 ? 4 : (n >= 512 ? 2 : 1);
+    const uint64_t grid = (total + 1024 * I - 1) / (1024 * I);
+    if (grid > 0x7fffffffull) return hipErrorInvalidValue;
+    if (I == 4)
+      hipLaunchKernelGGL(mfa_hadamard_wave_kernel<4>, dim3((unsigned)grid), dim3(256), 0, stream,
+                         data, log2n, total, scale);
+    else if (I == 2)
+      hipLaunchKernelGGL(mfa_hadamard_wave_kernel<2>, dim3((unsigned)grid), dim3(256), 0, stream,
+                         data, log2n, total, scale);
+    else
+      hipLaunchKernelGGL(mfa_hadamard_wave_kernel<1>, dim3((unsigned)grid), dim3(256), 0, stream,
+                         data, log2n, total, scale);
+    return hipGetLastError();
+  }
+  const int R = (int)n;  // 1 or 2
   const uint64_t threads = total / R;
   const uint64_t grid = (threads + 255) / 256;
   if (grid > 0x7fffffffull) return hipErrorInvalidValue;
@@ -94,7 +175,7 @@ hipError_t hadamard_dispatch(float* data, int log2n, uint64_t num_blocks, float 
     hipLaunchKernelGGL(mfa_hadamard_kernel<RR>, dim3((unsigned)grid), dim3(256), 0, stream, \
                        data, log2n, total, scale);                                         \
     break;
-    MFA_HAD(1) MFA_HAD(2) MFA_HAD(4) MFA_HAD(8) MFA_HAD(16)
+    MFA_HAD(1) MFA_HAD(2)
 #undef MFA_HAD
     default: return hipErrorInvalidValue;
   }
