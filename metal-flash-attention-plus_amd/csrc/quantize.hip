@@ -158,7 +158,19 @@ __global__ void __launch_bounds__(256) qz_absmax_tensor_v(const void* in, uint64
   float m = 0.f;
   const uint64_t n8 = n / 8, stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  for (uint64_t v = gid; v < n8; v += stride) {
+  // Four grid-stride steps' loads in flight at a time (one step at a time is a chain of HBM
+  // latencies: 3.2 TB/s at 16.8 M FP32 elements).
+  uint64_t v = gid;
+  for (; v + 3 * stride < n8; v += 4 * stride) {
+    float x[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8<PREC>(in, v + u * stride, x[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(x[u][k]));
+  }
+  for (; v < n8; v += stride) {
     float x[8];
     load8<PREC>(in, v, x);
 #pragma unroll
@@ -168,23 +180,45 @@ __global__ void __launch_bounds__(256) qz_absmax_tensor_v(const void* in, uint64
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
+  // One partial per workgroup (no atomics, so no workspace reset launch): the quantise kernel
+  // reduces them.
   if (threadIdx.x == 0)
-    atomicMax(ws, abs_bits(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    ws[blockIdx.x] = abs_bits(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 // MODE 0 tensor-wise, 1 block-wise, 2 row-wise; requires cols % 8 == 0 (and bs % 8 == 0 for
 // block-wise) so that the 8 elements of a step share one scale.
+// Tensor-wise (MODE 0) with `ws`: every workgroup reduces qz_absmax_tensor_v's nws partial
+// maxima (float bits of |x|, compared as unsigned like the atomicMax of the scalar path) and
+// computes the scale absmax / div, as qz_scale_tensor does; thread 0 of the grid also stores it
+// to scale_t.
 template <int PREC, int TARGET, int MODE>
 __global__ void __launch_bounds__(256) qz_quantize_v(const void* in, uint64_t n, uint32_t cols,
                                                      uint32_t bs, uint32_t nbc,
                                                      const float* scale_t, const float* scales,
-                                                     uint8_t* out) {
+                                                     uint8_t* out, const unsigned* ws, int nws,
+                                                     float div) {
   const uint64_t n8 = n / 8, stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  const float st = MODE == 0 ? scale_t[0] : 0.f;
-  for (uint64_t v = gid; v < n8; v += stride) {
-    float x[8];
-    load8<PREC>(in, v, x);
+  float st = 0.f;
+  if constexpr (MODE == 0) {
+    if (ws) {
+      __shared__ unsigned wred[4];
+      unsigned mb = 0u;
+      for (int i = threadIdx.x; i < nws; i += 256) mb = max(mb, ws[i]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+      if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = mb;
+      __syncthreads();
+      mb = max(max(wred[0], wred[1]), max(wred[2], wred[3]));
+      st = __builtin_bit_cast(float, mb) / div;
+      if (gid == 0) const_cast<float*>(scale_t)[0] = st;
+    } else {
+      st = scale_t[0];
+    }
+  }
+  // One 8-element step: quantise x and store.
+  auto step = [&](uint64_t v, const float (&x)[8]) {
     float s = st;
     if constexpr (MODE != 0) {
       const uint64_t i = v * 8, r = i / cols, c = i % cols;
@@ -202,6 +236,11 @@ __global__ void __launch_bounds__(256) qz_quantize_v(const void* in, uint64_t n,
       for (int k = 0; k < 8; ++k) w |= nib((int64_t)round_to_int(x[k] / s) + 8) << (4 * k);
       reinterpret_cast<uint32_t*>(out)[v] = w;
     }
+  };
+  for (uint64_t v = gid; v < n8; v += stride) {
+    float x[8];
+    load8<PREC>(in, v, x);
+    step(v, x);
   }
   // Tail (n % 8 elements), element by element as in qz_quantize.
   const uint64_t i0 = n8 * 8;
@@ -293,34 +332,40 @@ void launch_absmax_v(const void* in, uint64_t n, unsigned* ws, hipStream_t s) {
 template <int PREC, int TARGET>
 void launch_quantize_v(int mode, const void* in, uint64_t n, uint32_t cols, uint32_t bs,
                        uint32_t nbc, const float* st, const float* sc, uint8_t* out,
-                       hipStream_t s) {
+                       const unsigned* ws, float div, hipStream_t s) {
   const dim3 g(grid_vec(n)), b(256);
+  const int nws = grid_vec(n);  // qz_absmax_tensor_v's grid: one partial per workgroup
   if (mode == 0)
-    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 0>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out);
+    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 0>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out, ws, nws, div);
   else if (mode == 1)
-    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 1>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out);
+    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 1>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out, ws, nws, div);
   else
-    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 2>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out);
+    hipLaunchKernelGGL((mfa::qz_quantize_v<PREC, TARGET, 2>), g, b, 0, s, in, n, cols, bs, nbc, st, sc, out, ws, nws, div);
 }
 template <int PREC>
 void launch_quantize_vp(int target, int mode, const void* in, uint64_t n, uint32_t cols,
                         uint32_t bs, uint32_t nbc, const float* st, const float* sc, uint8_t* out,
-                        hipStream_t s) {
+                        const unsigned* ws, float div, hipStream_t s) {
   if (target == mfa::P_INT8)
-    launch_quantize_v<PREC, mfa::P_INT8>(mode, in, n, cols, bs, nbc, st, sc, out, s);
+    launch_quantize_v<PREC, mfa::P_INT8>(mode, in, n, cols, bs, nbc, st, sc, out, ws, div, s);
   else
-    launch_quantize_v<PREC, mfa::P_INT4>(mode, in, n, cols, bs, nbc, st, sc, out, s);
+    launch_quantize_v<PREC, mfa::P_INT4>(mode, in, n, cols, bs, nbc, st, sc, out, ws, div, s);
 }
-// Vector quantise when the layout allows it; false: use the scalar kernel.
-bool quantize_vec(int prec, int target, int mode, const void* in, uint64_t n, uint32_t cols,
-                  uint32_t bs, uint32_t nbc, const float* st, const float* sc, uint8_t* out,
-                  hipStream_t s) {
+bool quantize_vec_ok(int target, int mode, const void* in, uint32_t cols, uint32_t bs,
+                     const uint8_t* out) {
   if (!aligned16(in)) return false;
   if (((uintptr_t)out & (target == mfa::P_INT8 ? 7 : 3)) != 0) return false;
-  if (mode != 0 && (cols % 8 != 0 || (mode == 1 && bs % 8 != 0))) return false;
-  if (prec == mfa::P_FP32) launch_quantize_vp<mfa::P_FP32>(target, mode, in, n, cols, bs, nbc, st, sc, out, s);
-  else if (prec == mfa::P_FP16) launch_quantize_vp<mfa::P_FP16>(target, mode, in, n, cols, bs, nbc, st, sc, out, s);
-  else launch_quantize_vp<mfa::P_BF16>(target, mode, in, n, cols, bs, nbc, st, sc, out, s);
+  return !(mode != 0 && (cols % 8 != 0 || (mode == 1 && bs % 8 != 0)));
+}
+// Vector quantise when the layout allows it; false: use the scalar kernel.  With `ws` (tensor-
+// wise only) the kernel derives the scale from the absmax bits and writes it to `st`.
+bool quantize_vec(int prec, int target, int mode, const void* in, uint64_t n, uint32_t cols,
+                  uint32_t bs, uint32_t nbc, const float* st, const float* sc, uint8_t* out,
+                  hipStream_t s, const unsigned* ws = nullptr, float div = 1.f) {
+  if (!quantize_vec_ok(target, mode, in, cols, bs, out)) return false;
+  if (prec == mfa::P_FP32) launch_quantize_vp<mfa::P_FP32>(target, mode, in, n, cols, bs, nbc, st, sc, out, ws, div, s);
+  else if (prec == mfa::P_FP16) launch_quantize_vp<mfa::P_FP16>(target, mode, in, n, cols, bs, nbc, st, sc, out, ws, div, s);
+  else launch_quantize_vp<mfa::P_BF16>(target, mode, in, n, cols, bs, nbc, st, sc, out, ws, div, s);
   return true;
 }
 }  // namespace
@@ -328,7 +373,9 @@ bool quantize_vec(int prec, int target, int mode, const void* in, uint64_t n, ui
 extern "C" size_t mfa_quantize_workspace_size(uint64_t count, uint32_t rows, uint32_t cols,
                                               int32_t mode, uint32_t block_size) {
   (void)count; (void)rows; (void)cols; (void)block_size;
-  return mode == MFA_QUANT_TENSOR_WISE ? 16 : 0;
+  // Tensor-wise: one absmax partial per workgroup of the vector kernels (at most 1024), or the
+  // scalar path's single atomic word.
+  return mode == MFA_QUANT_TENSOR_WISE ? 4096 : 0;
 }
 
 extern "C" mfa_status_t mfa_quantize(const void* input, int32_t input_precision, uint64_t count,
@@ -349,8 +396,11 @@ extern "C" mfa_status_t mfa_quantize(const void* input, int32_t input_precision,
   if (count == 0) return MFA_SUCCESS;
   if (mode == MFA_QUANT_TENSOR_WISE) {
     if (!workspace || !scale_out) return MFA_ERR_INVALID_ARGUMENT;
-    if (hipMemsetAsync(workspace, 0, 16, s) != hipSuccess) return MFA_ERR_LAUNCH;
-    if (aligned16(input)) {
+    const bool vec = aligned16(input) &&
+                     quantize_vec_ok(target_precision, 0, input, cols ? cols : 1u, 1u,
+                                     (const uint8_t*)output);
+    if (!vec && hipMemsetAsync(workspace, 0, 16, s) != hipSuccess) return MFA_ERR_LAUNCH;
+    if (vec) {
       if (input_precision == MFA_PRECISION_FP32)
         launch_absmax_v<P_FP32>(input, count, (unsigned*)workspace, s);
       else if (input_precision == MFA_PRECISION_FP16)
@@ -361,13 +411,15 @@ extern "C" mfa_status_t mfa_quantize(const void* input, int32_t input_precision,
       hipLaunchKernelGGL(qz_absmax_tensor, dim3(grid_for(count)), dim3(256), 0, s, input,
                          input_precision, count, (unsigned*)workspace);
     }
-    hipLaunchKernelGGL(qz_scale_tensor, dim3(1), dim3(64), 0, s, (const unsigned*)workspace,
-                       scale_out, div);
     if (!quantize_vec(input_precision, target_precision, 0, input, count, cols ? cols : 1u, 1u,
-                      1u, scale_out, nullptr, (uint8_t*)output, s))
+                      1u, scale_out, nullptr, (uint8_t*)output, s, (const unsigned*)workspace,
+                      div)) {
+      hipLaunchKernelGGL(qz_scale_tensor, dim3(1), dim3(64), 0, s, (const unsigned*)workspace,
+                         scale_out, div);
       hipLaunchKernelGGL(qz_quantize, dim3(grid_for(count)), dim3(256), 0, s, input,
                          input_precision, count, cols ? cols : 1u, target_precision, 0, 1u, 1u,
                          (const float*)scale_out, (const float*)nullptr, (uint8_t*)output);
+    }
   } else if (mode == MFA_QUANT_BLOCKWISE || mode == MFA_QUANT_ROW_WISE) {
     if (!block_scales_out || rows == 0 || cols == 0) return MFA_ERR_INVALID_ARGUMENT;
     uint32_t bsr, bsc, nbr, nbc;

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Runs one hot-path configuration a few times (a short program for rocprofv3 PMC passes).
-Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv,mla_dec} [reps]"""
+Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv,mla_dec,quant} [reps]"""
 import os
 import sys
 
@@ -25,6 +25,12 @@ if which in ("c2", "c3"):
     desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
     for _ in range(reps):
         mha.forward(desc, q, k, v, o, l)
+elif which == "quant":
+    # Runtime quantiser at the C3 K size (16.8 M FP32 elements): tensor-wise and row-wise INT8.
+    x = u((16 * 8192 * 128,), torch.float32)
+    for _ in range(reps):
+        mfa.quantize(x, mfa.Precision.INT8)
+        mfa.quantize(x, mfa.Precision.INT8, rows=16 * 8192, cols=128)
 elif which == "mla_dec":
     # Absorbed MLA decode, as bench.py's next_rows entry (B32 H16 S_q 1 S_kv 4096, latent 512).
     B, H, Sq, Skv, D, LAT = 32, 16, 1, 4096, 128, 512
