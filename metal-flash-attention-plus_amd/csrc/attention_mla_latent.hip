@@ -398,6 +398,88 @@ static hipError_t launch_latent(const LatentParams& p, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Decode query projection Q̃[b, h, :] = q[b, h, :] · W_k[:, h·D : (h+1)·D]ᵀ (S_q = 1): a workgroup
+// takes one head, QC latent columns and 32 batch rows; the W_k slice [QC][D] and the query rows
+// [32][D] sit in LDS (rows padded by 16 B), each thread accumulates QC/8 columns of one row in
+// FP32 over D.  Replaces a 128x128-tile GEMM launch whose 64 workgroups were mostly padding
+// (M = B rows per head).
+constexpr int QC = 16;
+template <class E>
+__global__ void __launch_bounds__(256) mfa_mla_qproj_kernel(const uint16_t* __restrict__ q,
+                                                            const uint16_t* __restrict__ wk,
+                                                            uint16_t* __restrict__ qt, int B,
+                                                            int H, int D, int Lat) {
+  constexpr int NJ = QC / 8;  // columns per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int RS = D * 2 + 16;  // padded row stride (bytes)
+  char* const wsl = smem;            // [QC][RS]
+  char* const qsl = smem + QC * RS;  // [32][RS]
+  const int h = blockIdx.x, l0 = blockIdx.y * QC, b0 = blockIdx.z * 32;
+  const int tid = threadIdx.x;
+  const int cpr = D / 8;  // 16-byte chunks per row
+  for (int i = tid; i < QC * cpr; i += 256) {
+    const int r = i / cpr, c = i % cpr;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (l0 + r < Lat)
+      v = *reinterpret_cast<const uint4*>(wk + (int64_t)(l0 + r) * H * D + (int64_t)h * D + 8 * c);
+    *reinterpret_cast<uint4*>(wsl + r * RS + 16 * c) = v;
+  }
+  for (int i = tid; i < 32 * cpr; i += 256) {
+    const int r = i / cpr, c = i % cpr;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (b0 + r < B) v = *reinterpret_cast<const uint4*>(q + ((int64_t)(b0 + r) * H + h) * D + 8 * c);
+    *reinterpret_cast<uint4*>(qsl + r * RS + 16 * c) = v;
+  }
+  __syncthreads();
+  const int br = tid >> 3, lg = tid & 7;
+  float acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = 0.f;
+  for (int c = 0; c < cpr; ++c) {
+    const uint4 qv = *reinterpret_cast<const uint4*>(qsl + br * RS + 16 * c);
+    float qf[8];
+    const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qf[2 * e] = E::to_f32((uint16_t)(qw[e] & 0xffffu));
+      qf[2 * e + 1] = E::to_f32((uint16_t)(qw[e] >> 16));
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const uint4 wv = *reinterpret_cast<const uint4*>(wsl + (lg * NJ + j) * RS + 16 * c);
+      const uint32_t ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[j] = __builtin_fmaf(qf[2 * e], E::to_f32((uint16_t)(ww[e] & 0xffffu)), acc[j]);
+        acc[j] = __builtin_fmaf(qf[2 * e + 1], E::to_f32((uint16_t)(ww[e] >> 16)), acc[j]);
+      }
+    }
+  }
+  const int b = b0 + br;
+  if (b >= B) return;
+  uint16_t* orow = qt + ((int64_t)b * H + h) * Lat + l0 + lg * NJ;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    if (l0 + lg * NJ + j < Lat) orow[j] = E::from_f32(acc[j]);
+}
+
+hipError_t mla_qproj_dispatch(const void* q, const void* wk, void* qt, int B, int H, int D,
+                              int Lat, int elem, hipStream_t stream) {
+  if (D % 8 != 0 || D > 256 || ((uintptr_t)q & 15) || ((uintptr_t)wk & 15))
+    return hipErrorNotSupported;
+  const dim3 grid(H, (Lat + QC - 1) / QC, (B + 31) / 32);
+  const size_t lds = (size_t)(QC + 32) * (D * 2 + 16);
+  if (elem == P_FP16)
+    hipLaunchKernelGGL(mfa_mla_qproj_kernel<F16>, grid, dim3(256), lds, stream,
+                       (const uint16_t*)q, (const uint16_t*)wk, (uint16_t*)qt, B, H, D, Lat);
+  else if (elem == P_BF16)
+    hipLaunchKernelGGL(mfa_mla_qproj_kernel<BF16>, grid, dim3(256), lds, stream,
+                       (const uint16_t*)q, (const uint16_t*)wk, (uint16_t*)qt, B, H, D, Lat);
+  else
+    return hipErrorNotSupported;
+  return hipGetLastError();
+}
+
 hipError_t mla_latent_dispatch(const LatentParams& p, int elem, int lat, hipStream_t stream) {
   if (lat == 512 && elem == P_FP16) return launch_latent<F16, 512>(p, stream);
   if (lat == 512 && elem == P_BF16) return launch_latent<BF16, 512>(p, stream);

@@ -1033,9 +1033,13 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
   // weight slice is read once (M = B) instead of once per batch item.
   const bool decode = Sq == 1 && B > 1;
   if (decode) {
-    if ((st = general(query, w_k, qt, B, Lat, D, H * D, H * Lat, 1, prec, D, Lat, H, 0)) !=
-        MFA_SUCCESS)
+    const hipError_t e = mfa::mla_qproj_dispatch(query, w_k, qt, B, H, D, Lat, elem_of(prec), s);
+    if (e != hipErrorNotSupported) {
+      if ((st = hip_status(e, "absorbed MLA query projection launch")) != MFA_SUCCESS) return st;
+    } else if ((st = general(query, w_k, qt, B, Lat, D, H * D, H * Lat, 1, prec, D, Lat, H,
+                             0)) != MFA_SUCCESS) {
       return st;
+    }
   } else if (B > 1) {
     if ((st = general(query, w_k, qt, Sq, Lat, D, D, Lat, 1, prec, (int64_t)Sq * D,
                       (int64_t)Sq * Lat, B * H, H)) != MFA_SUCCESS)

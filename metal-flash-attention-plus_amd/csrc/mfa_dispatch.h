@@ -61,6 +61,10 @@ hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream);
 // MLA latent-space attention (attention_mla_latent.hip); lat = 256 or 512.
 hipError_t mla_latent_dispatch(const LatentParams& p, int elem, int lat, hipStream_t stream);
+// Decode (S_q = 1) query projection of the absorbed MLA path; hipErrorNotSupported when the
+// shapes or alignment do not fit (the caller falls back to the general GEMM).
+hipError_t mla_qproj_dispatch(const void* q, const void* wk, void* qt, int B, int H, int D,
+                              int Lat, int elem, hipStream_t stream);
 // General GEMMDescriptor surface (gemm_general.hip); compute precision chosen from A and B.
 int gemm_general_compute(int prec_a, int prec_b);
 hipError_t gemm_general_dispatch(const GemmGParams& p, int batch, hipStream_t stream);
