@@ -60,6 +60,20 @@ def test_runtime_quantize_rowwise_scales(gpu):
         assert np.array_equal(q[r], ol.quantize(x[r], int(P.INT8), s_ref[r]).view(np.int8))
 
 
+def test_runtime_quantize_tensorwise_partials_not_stale(gpu):
+    # The tensor-wise vector path leaves one absmax partial per workgroup in the workspace and
+    # the quantise kernel reduces them: a large-magnitude tensor, then smaller tensors (fewer
+    # workgroups, smaller maxima) on recycled workspace memory must each get their own scale.
+    sizes = [(1 << 22, 40.0), (1 << 16, 0.5), (1 << 20, 3.0), (4096, 0.01)]
+    for i, (n, amp) in enumerate(sizes):
+        x = (np.random.default_rng(20 + i).standard_normal(n) * amp).astype(np.float32)
+        data, scale, _, _ = mfa.quantize(torch.from_numpy(x).cuda(), P.INT8)
+        torch.cuda.synchronize()
+        s_ref = ol.quant_scale_tensor(x, int(P.INT8))
+        assert scale.item() == np.float32(s_ref), (n, amp)
+        assert np.array_equal(data.cpu().numpy(), ol.quantize(x, int(P.INT8), s_ref))
+
+
 @pytest.mark.parametrize("target", [P.INT8, P.INT4])
 @pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
 def test_runtime_quantize_large_vector_paths(gpu, target, src):
