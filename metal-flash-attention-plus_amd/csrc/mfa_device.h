@@ -314,6 +314,13 @@ __device__ __forceinline__ float cross_half_max(float x) {
                                                   __builtin_bit_cast(unsigned, x), false, false);
   return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
 }
+// The same with IEEE maximum (v_maximum_f32: no operand canonicalisation; NaN propagates).
+__device__ __forceinline__ float cross_half_maximum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                                  __builtin_bit_cast(unsigned, x), false, false);
+  return __builtin_elementwise_maximum(__builtin_bit_cast(float, (unsigned)r[0]),
+                                       __builtin_bit_cast(float, (unsigned)r[1]));
+}
 __device__ __forceinline__ float cross_half_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
                                                   __builtin_bit_cast(unsigned, x), false, false);

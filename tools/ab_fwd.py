@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--cfg", default="C2")
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--nocheck", action="store_true", help="timing-only variants (ablations)")
     a = ap.parse_args()
     var, vals = a.knob.split("=")
     vals = vals.split(",")
@@ -66,7 +67,7 @@ def main():
                 ref = o.clone()
             elif i8:
                 rel[x] = float((o - ref).norm() / ref.norm())
-            else:
+            elif not a.nocheck:
                 assert torch.allclose(o, ref, atol=2e-3), f"{var}={x} differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
