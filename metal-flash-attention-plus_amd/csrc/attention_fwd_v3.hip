@@ -50,7 +50,6 @@ constexpr int TILEB = BK * DP * 2;  // one K or V tile: 16 KiB
 constexpr int KSLOTS = 5, VSLOTS = 4;
 constexpr int LDS_BYTES = (KSLOTS + VSLOTS) * TILEB;  // 144 KiB
 constexpr int NM = 16;                                // MFMAs per phase (either product)
-constexpr int NP = 6;                                 // fragments read ahead
 constexpr float THR = 8.0f;
 using DMA = DmaA<DP, BK, 256>;
 
@@ -101,14 +100,14 @@ __device__ __forceinline__ f32x16 mfma_first(const i16x8& a, const i16x8& b, con
 // DMA offsets into AGPRs and reload them before every use); as inline asm, O lives in AGPRs
 // (only the PV chain and the rare rescale touch it) while S stays in VGPRs for the softmax.
 // hipcc does not pad hazards inside asm: the leading s_nop covers a VALU write of P (or an
-// AGPR write of O) right before the MFMA (2 wait states needed, 5 given); O is read back by
+// AGPR write of O) right before the MFMA (2 wait states needed, 3 given); O is read back by
 // VALU only after mfma_drain() or a barrier plus an MFMA phase.
 template <class E>
 __device__ __forceinline__ void mfma_acc_a(f32x16& acc, const i16x8& a, const i16x8& b) {
   if constexpr (E::prec == P_FP16)
-    asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else
-    asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 // Covers the MFMA -> VALU read latency of an asm MFMA's accumulator (16 passes).
 __device__ __forceinline__ void mfma_drain() {
@@ -140,11 +139,14 @@ struct VFrag {
 // S^T = K·Q^T (16 MFMAs): key on the MFMA row (registers), query on the lane.  i0 / i1 are
 // the initial accumulators of keys 0-31 / 32-63 (−m, or 0 for bf16; −inf where masked).
 // cur: this phase's first NP fragments (read by the previous phase); nxt <- the next
-// phase's first NP fragments, read in this phase's last MFMA gaps.
-template <class E, class Next>
+// phase's first NP fragments, read in this phase's last MFMA gaps.  slot(i) issues the VALU
+// work placed in MFMA gap i (a slice of the other stream's softmax); every gap is closed by a
+// full scheduling barrier, so the interleave is exactly the source order (hipcc, left to
+// itself, clusters the softmax VALU and leaves the matrix pipe idle between MFMA runs).
+template <class E, int NP, class Next, class Slot>
 __device__ __forceinline__ void qk(Stream& st, const KFrag<E>& rd, const i16x8 (&qf)[DS],
                                    const f32x16& i0, const f32x16& i1, i16x8 (&cur)[NP],
-                                   i16x8 (&nxt)[NP], const Next& rdn) {
+                                   i16x8 (&nxt)[NP], const Next& rdn, Slot&& slot) {
   using A = Arith16<E, DP>;
 #pragma unroll
   for (int i = 0; i < NM; ++i) {
@@ -157,14 +159,17 @@ __device__ __forceinline__ void qk(Stream& st, const KFrag<E>& rd, const i16x8 (
       cur[i % NP] = rd(i + NP);
     else
       nxt[i + NP - NM] = rdn(i + NP - NM);
-    pin_mem_order();
+    slot(i);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  slot(NM);  // the pipelined slices' last stage, right behind the chain
+  __builtin_amdgcn_sched_barrier(0);
 }
 
-// O^T += V^T·P^T (16 MFMAs), same fragment pipeline.
-template <class E, class Next>
+// O^T += V^T·P^T (16 MFMAs), same fragment pipeline and gap slots (slot(i), i < 16).
+template <class E, int NP, class Next, class Slot>
 __device__ __forceinline__ void pv(Stream& st, const VFrag<E>& rd, i16x8 (&cur)[NP],
-                                   i16x8 (&nxt)[NP], const Next& rdn) {
+                                   i16x8 (&nxt)[NP], const Next& rdn, Slot&& slot) {
 #pragma unroll
   for (int i = 0; i < NM; ++i) {
     const int jk = i / ND, dt = i % ND;
@@ -173,8 +178,68 @@ __device__ __forceinline__ void pv(Stream& st, const VFrag<E>& rd, i16x8 (&cur)[
       cur[i % NP] = rd(i + NP);
     else
       nxt[i + NP - NM] = rdn(i + NP - NM);
-    pin_mem_order();
+    slot(i);
+    __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+// Two fp32 values rounded to one packed 16-bit pair (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32).
+template <class E>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  if constexpr (E::prec == P_FP16) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{a, b}, h2));
+  } else {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{a, b}, b2));
+  }
+}
+
+// Slice i (0..16) of a stream's softmax for one MFMA gap, software-pipelined by one gap so
+// nothing waits on the transcendental latency: P = exp2(S') of elements 2i, 2i+1 (i < 16),
+// then the 16-bit pack (one operand word) and the row-sum share (two partial sums) of the
+// pair exponentiated in the previous gap (i > 0).
+template <class E, bool PS>
+__device__ __forceinline__ void expo_slice(Stream& st, float c, int i, float (&rs)[2]) {
+  if (i < 16) {
+    const int j = i / 8, e = 2 * (i % 8);
+    float x0 = st.s[j][e], x1 = st.s[j][e + 1];
+    if constexpr (!PS) {
+      x0 = __builtin_fmaf(x0, c, -st.m);
+      x1 = __builtin_fmaf(x1, c, -st.m);
+    }
+    st.s[j][e] = __builtin_amdgcn_exp2f(x0);
+    st.s[j][e + 1] = __builtin_amdgcn_exp2f(x1);
+  }
+  if (i > 0) {
+    const int h = i - 1, j = h / 8, e = 2 * (h % 8);
+    const float p0 = st.s[j][e], p1 = st.s[j][e + 1];
+    rs[0] += p0;
+    rs[1] += p1;
+    const int jk = j * 2 + (h % 8) / 4, w = h % 4;
+    const uint32_t word = pack2<E>(p0, p1);
+    uint4 v = __builtin_bit_cast(uint4, st.pb[jk]);
+    if (w == 0) v.x = word;
+    if (w == 1) v.y = word;
+    if (w == 2) v.z = word;
+    if (w == 3) v.w = word;
+    st.pb[jk] = __builtin_bit_cast(i16x8, v);
+  }
+}
+
+// Slice i (0..15) of a stream's row max: elements 2i, 2i+1 into one of four maximum chains.
+__device__ __forceinline__ void max_slice(const Stream& st, int i, float (&r)[4]) {
+  const int j = i / 8, e = 2 * (i % 8), k = i % 4;
+  const float a = st.s[j][e], b = st.s[j][e + 1];
+  r[k] = i < 4 ? __builtin_elementwise_maximum(a, b)
+               : __builtin_elementwise_maximum(r[k], __builtin_elementwise_maximum(a, b));
+}
+template <bool PS>
+__device__ __forceinline__ float max_final(const Stream& st, const float (&r)[4], float c) {
+  const float mx = cross_half_maximum(__builtin_elementwise_maximum(
+      __builtin_elementwise_maximum(r[0], r[1]), __builtin_elementwise_maximum(r[2], r[3])));
+  return PS ? mx + st.moff : mx * c;
 }
 
 // Tile max of the lane's row in absolute log2 units (both halves).
@@ -319,9 +384,42 @@ __device__ __forceinline__ void store_stream(const FwdParams& p, const f32x16 (&
 
 template <int V> using IC = std::integral_constant<int, V>;
 
-template <class E, bool CAUSAL>
+// Diagnostic build only (tools/diag/v3_stamps.hip defines V3_STAMPS): per-wave shader-cycle
+// totals of the iteration's segments, into a buffer no kernel output is computed from.
+#ifdef V3_STAMPS
+__device__ unsigned long long g_v3_stamps[1 << 16][8];
+#define V3_SEG_DECL() unsigned long long seg_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, segt_ = v3_clock()
+#define V3_SEG(k)                          \
+  do {                                     \
+    const unsigned long long t_ = v3_clock(); \
+    seg_[k] += t_ - segt_;                 \
+    segt_ = t_;                            \
+  } while (0)
+#define V3_SEG_END()                                                                 \
+  do {                                                                               \
+    if ((threadIdx.x & 63) == 0)                                                     \
+      for (int k_ = 0; k_ < 8; ++k_)                                                 \
+        g_v3_stamps[blockIdx.x * 4 + (threadIdx.x >> 6)][k_] = seg_[k_];             \
+  } while (0)
+__device__ __forceinline__ unsigned long long v3_clock() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#else
+#define V3_SEG_DECL() do {} while (0)
+#define V3_SEG(k) do {} while (0)
+#define V3_SEG_END() do {} while (0)
+#endif
+
+// TUNE (development A/B): 0 = shipped; 1 = steady-state DMA spread over M3 and M4;
+// 2 = no DMA in the steady loop (timing ablation, wrong results); 3 = 8 fragments read ahead.
+template <class E, bool CAUSAL, int TUNE = 0>
 __global__ void __launch_bounds__(256, 1) mfa_fwd3_kernel(FwdParams p) {
   constexpr bool PS = E::prec == P_FP16;
+  constexpr int NP = TUNE == 3 ? 8 : 6;  // fragments read ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const kring = smem;
   char* const vring = smem + KSLOTS * TILEB;
@@ -423,6 +521,7 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd3_kernel(FwdParams p) {
   // One pipelined iteration.  TIL: tiles per iteration in this loop (1 phase 1, 2 phase 2;
   // fixes the DMA issue count of the steady state), -1 = decided at run time.  MASKS: 0 = no
   // tile of the iteration is masked (no mask code at all), 1 = masks decided at run time.
+  V3_SEG_DECL();
   auto iter = [&](auto til_c, auto masks_c, const i16x8(&qa)[DS], int j, int q0a, int qia) {
     constexpr int TIL = decltype(til_c)::value;
     constexpr bool MASKS = decltype(masks_c)::value != 0;
@@ -436,52 +535,88 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd3_kernel(FwdParams p) {
     const VFrag<E> vBp{vslot(tbp), trb}, vA{vslot(ta), trb};
 
     // ---- M1: S_A = K·Q_A^T | exp, row sum, pack of B's previous tile; reads for M2
+    float rsb[2] = {0.f, 0.f};
+    auto m1 = [&](int i) { expo_slice<E, PS>(sb, c, i, rsb); };
     if (MASKS && needs_mask(ta, q0a)) {
       f32x16 i0, i1;
       masked_init<PS>(sa, hi_of(ta, qia), i0, i1);
-      qk<E>(sa, kA, qa, i0, i1, kf, vf, vBp);
+      qk<E, NP>(sa, kA, qa, i0, i1, kf, vf, vBp, m1);
     } else {
-      qk<E>(sa, kA, qa, PS ? sa.negm : zero16(), PS ? sa.negm : zero16(), kf, vf, vBp);
+      qk<E, NP>(sa, kA, qa, PS ? sa.negm : zero16(), PS ? sa.negm : zero16(), kf, vf, vBp, m1);
     }
-    expo<E, PS>(sb, c);
+    sb.lh += rsb[0] + rsb[1];
+    V3_SEG(6);
     // ---- M2: O_B += V·P_B^T (B's previous tile) | row max of A; reads for M3
-    pv<E>(sb, vBp, vf, kf, kB);
+    float ra[4];
+    pv<E, NP>(sb, vBp, vf, kf, kB, [&](int i) { max_slice(sa, i, ra); });
     if constexpr (MASKS) mfma_drain();
-    const float mta = rowmax<PS>(sa, c);
+    const float mta = max_final<PS>(sa, ra, c);
+    V3_SEG(0);
     // Tiles issued in the previous iteration's M4 have landed (every wave's own pieces), and
     // after the barrier every wave has passed M2: their slots may be refilled in M4 below.
     wait_vm();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
+    V3_SEG(1);
     rescale<PS>(sa, mta);
+    V3_SEG(2);
 
     // ---- M3: S_B = K·Q_B^T | exp, row sum, pack of A; reads for M4
+    float rsa[2] = {0.f, 0.f};
+    auto m3 = [&](int i) {
+      expo_slice<E, PS>(sa, c, i, rsa);
+      if constexpr (TUNE == 1 && TIL == 1) {
+        if (i % 4 == 2) kd.issue_piece(khead, (j + 2) * BK, kslot(j + 2), i / 4);
+      }
+    };
     if (MASKS && needs_mask(tb, q0Y)) {
       f32x16 i0, i1;
       masked_init<PS>(sb, hi_of(tb, qiY), i0, i1);
-      qk<E>(sb, kB, qY, i0, i1, kf, vf, vA);
+      qk<E, NP>(sb, kB, qY, i0, i1, kf, vf, vA, m3);
     } else {
-      qk<E>(sb, kB, qY, PS ? sb.negm : zero16(), PS ? sb.negm : zero16(), kf, vf, vA);
+      qk<E, NP>(sb, kB, qY, PS ? sb.negm : zero16(), PS ? sb.negm : zero16(), kf, vf, vA, m3);
     }
-    expo<E, PS>(sa, c);
-    // ---- M4: O_A += V·P_A^T | row max of B; reads for the next M1; DMA
-    if constexpr (TIL == 1) {
-      vd.issue(vhead, (j + 1) * BK, vslot(j + 1));
-      kd.issue(khead, (j + 2) * BK, kslot(j + 2));
+    sa.lh += rsa[0] + rsa[1];
+    V3_SEG(7);
+    // ---- M4: O_A += V·P_A^T | row max of B; reads for the next M1; DMA (V of j+1, K of j+2)
+    float rb[4];
+    if constexpr (TIL == 1 && (TUNE == 1 || TUNE == 2)) {
+      // TUNE 1: the K half of the DMA went into M3's gaps (below the QK^T call).
+      pv<E, NP>(sa, vA, vf, kf, kN, [&](int i) {
+        max_slice(sb, i, rb);
+        if (TUNE == 1 && i % 4 == 2) vd.issue_piece(vhead, (j + 1) * BK, vslot(j + 1), i / 4);
+      });
+    } else if constexpr (TIL == 1) {
+      // One DMA piece in every other gap.
+      pv<E, NP>(sa, vA, vf, kf, kN, [&](int i) {
+        max_slice(sb, i, rb);
+        if (i % 2 == 0) {
+          if (i < 2 * DMA::PPW)
+            vd.issue_piece(vhead, (j + 1) * BK, vslot(j + 1), i / 2);
+          else
+            kd.issue_piece(khead, (j + 2) * BK, kslot(j + 2), i / 2 - DMA::PPW);
+        }
+      });
     } else if constexpr (TIL == 2) {
       const int a1 = ta_of(j + 1), a2 = ta_of(j + 2);
-      vd.issue(vhead, a1 * BK, vslot(a1));
-      vd.issue(vhead, (a1 + 1) * BK, vslot(a1 + 1));
-      kd.issue(khead, a2 * BK, kslot(a2));
-      kd.issue(khead, (a2 + 1) * BK, kslot(a2 + 1));
+      pv<E, NP>(sa, vA, vf, kf, kN, [&](int i) {
+        max_slice(sb, i, rb);
+        const int q = i % DMA::PPW, t = i / DMA::PPW;
+        if (t == 0) vd.issue_piece(vhead, a1 * BK, vslot(a1), q);
+        if (t == 1) vd.issue_piece(vhead, (a1 + 1) * BK, vslot(a1 + 1), q);
+        if (t == 2) kd.issue_piece(khead, a2 * BK, kslot(a2), q);
+        if (t == 3) kd.issue_piece(khead, (a2 + 1) * BK, kslot(a2 + 1), q);
+      });
     } else {
       issue_v(j + 1);
       issue_k(j + 2);
+      pv<E, NP>(sa, vA, vf, kf, kN, [&](int i) { max_slice(sb, i, rb); });
     }
-    pv<E>(sa, vA, vf, kf, kN);
     if constexpr (MASKS) mfma_drain();  // generic bodies end in branches and joins
-    const float mtb = rowmax<PS>(sb, c);
+    const float mtb = max_final<PS>(sb, rb, c);
+    V3_SEG(3);
     rescale<PS>(sb, mtb);
+    V3_SEG(4);
   };
 
   // Masked tiles (causal diagonal, the key edge, phase 2's filler tile) only ever fall in the
@@ -506,13 +641,15 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd3_kernel(FwdParams p) {
     if (j < J) iter(IC<-1>(), IC<1>(), qY, j++, q0Y, qiY);
     if (j < J) iter(IC<-1>(), IC<1>(), qY, j++, q0Y, qiY);
   }
+  V3_SEG(5);
+  V3_SEG_END();
   // B's last tile.
   if (J > 0) {
     expo<E, PS>(sb, c);
     const VFrag<E> vB{vslot(tb_of(J - 1)), trb};
 #pragma unroll
     for (int k = 0; k < NP; ++k) vf[k] = vB(k);
-    pv<E>(sb, vB, vf, kf, vB);
+    pv<E, NP>(sb, vB, vf, kf, vB, [](int) {});
   }
   mfma_drain();
   if (CAUSAL) {
@@ -551,20 +688,28 @@ static hipError_t set_lds_attr_once(K kern, int bytes) {
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd3_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   if (DP != 128 || p.mask.window) return hipErrorNotSupported;
-  if (const char* e = getenv("MFA_FWD3")) {
-    if (e[0] == '0') return hipErrorNotSupported;
-  }
+  // Opt-in until it beats the v2 kernels (MFA_FWD3=1).
+  const char* e3 = getenv("MFA_FWD3");
+  if (!e3 || e3[0] != '1') return hipErrorNotSupported;
   FwdParams q = p;
   const int nb128 = (p.R + 127) / 128;
   q.nblk = p.mask.causal ? (nb128 + 1) / 2 : (p.R + 255) / 256;
   const dim3 grid(q.nblk * p.B * p.H), block(256);
-#define MFA_F3(EE, CA)                                                         \
+  static const int tune = getenv("MFA_V3_TUNE") ? atoi(getenv("MFA_V3_TUNE")) : 0;
+#define MFA_F3T(EE, CA, T)                                                     \
   {                                                                            \
-    auto kern = fwd3::mfa_fwd3_kernel<EE, CA>;                                 \
+    auto kern = fwd3::mfa_fwd3_kernel<EE, CA, T>;                              \
     hipError_t e = set_lds_attr_once(kern, fwd3::LDS_BYTES);                   \
     if (e != hipSuccess) return e;                                             \
     hipLaunchKernelGGL(kern, grid, block, fwd3::LDS_BYTES, stream, q);         \
     return hipGetLastError();                                                  \
+  }
+#define MFA_F3(EE, CA)                                                         \
+  {                                                                            \
+    if (tune == 1) MFA_F3T(EE, CA, 1)                                          \
+    if (tune == 2) MFA_F3T(EE, CA, 2)                                          \
+    if (tune == 3) MFA_F3T(EE, CA, 3)                                          \
+    MFA_F3T(EE, CA, 0)                                                         \
   }
   if (elem == P_FP16) {
     if (p.mask.causal) MFA_F3(F16, true) else MFA_F3(F16, false)
@@ -573,6 +718,7 @@ hipError_t fwd3_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
     if (p.mask.causal) MFA_F3(BF16, true) else MFA_F3(BF16, false)
   }
 #undef MFA_F3
+#undef MFA_F3T
   return hipErrorNotSupported;
 }
 

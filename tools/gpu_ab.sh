@@ -6,7 +6,7 @@ TAG=${1:-ab}; KNOB=${2:-MFA_FWD3=1,0}; CFGS=${3:-"C2 C3"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+${PYTEST_ENV:-} timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
     > "$OUT/pytest.log" 2>&1 || { echo "pytest failed rc=$?"; tail -40 "$OUT/pytest.log"; exit 1; }
 tail -2 "$OUT/pytest.log"
 for c in $CFGS; do
