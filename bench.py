@@ -72,6 +72,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def warm(fn, seconds=0.2):
+        """Time-based warm-up: repeat fn until `seconds` of back-to-back launches have run
+        (the clock settles over ~0.1 s from a cold chip), at least twice."""
+        fn()
+        torch.cuda.synchronize()
+        t, n = time.perf_counter(), 0
+        while n < 2 or time.perf_counter() - t < seconds:
+            fn()
+            n += 1
+            if n % 8 == 0 or n < 4:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+
+    def ev_time(fn, steps=20):
+        """HIP-event time per call on the current stream after a time-based warm-up;
+        at least 20 timed calls whatever --steps says."""
+        steps = max(20, steps)
+        warm(fn)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / steps
+
     import mfa_shard as shard
     H, S, D = args.heads, args.seq, args.dim
     B = 1  # per rank
@@ -113,28 +140,16 @@ def main():
         kh, vh = kf.half(), vf.half()
         desc3 = mfa.MultiHeadDescriptor.make(base3, B, H, S3, D)
 
-        def time_it(fn, steps):
-            for _ in range(2):
-                fn()
-            torch.cuda.synchronize()
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(steps):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            return e0.elapsed_time(e1) / steps
-
-        n3 = max(3, args.steps // 4)
-        ms_i8 = time_it(lambda: qa.forward(qdesc, tq, tk, tv, o3, l3, stream=stream), n3)
-        ms_i8x = time_it(lambda: qa.forward(qdesc_exact, tq, tk, tv, o3, l3, stream=stream), n3)
-        ms_f16 = time_it(lambda: mha.forward(desc3, qf, kh, vh, o3, l3, stream=stream), n3)
+        ms_i8 = ev_time(lambda: qa.forward(qdesc, tq, tk, tv, o3, l3, stream=stream))
+        ms_i8x = ev_time(lambda: qa.forward(qdesc_exact, tq, tk, tv, o3, l3, stream=stream))
+        ms_f16 = ev_time(lambda: mha.forward(desc3, qf, kh, vh, o3, l3, stream=stream))
         f3 = mfa.attention_flops(B, H, S3, S3, D, causal=False)
         result["int8"] = {
             "workload": "INT8 K/V (per-tensor, zp 0) + fp16 Q, H16 S8192 D128 non-causal "
                         "(BASELINE configs[2])",
-            "int8_kernel": "mfa_fwd_i8_kernel<F16,128,64> (i8 MFMA for QK^T and PV)",
+            "int8_kernel": mfa.quantized_plan(qdesc, mfa.KernelType.forward, tq, tk, tv)[0]["name"],
+            "int8_dequant_exact_kernel": mfa.quantized_plan(qdesc_exact, mfa.KernelType.forward,
+                                                            tq, tk, tv)[0]["name"],
             "int8_tops": round(f3 / (ms_i8 * 1e-3) / 1e12, 2),
             "int8_roofline_frac": round(f3 / (ms_i8 * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4),
             "fp16_tflops_same_shape": round(f3 / (ms_f16 * 1e-3) / 1e12, 2),
@@ -160,8 +175,8 @@ def main():
             mha.forward(desc5, q5, k5, v5, o5, l5, stream=stream)
             mha.backward(desc5, q5, k5, v5, o5, do5, l5, dq5, dk5, dv5, db5, stream=stream)
 
-        n5 = max(2, min(10, args.steps // 5))
-        step5()
+        n5 = 20
+        warm(step5)
         barrier()
         t5 = time.perf_counter()
         for _ in range(n5):
@@ -196,11 +211,10 @@ def main():
             mfa.mla_forward(base4, lat, wk, wv, q4, o4, B4, H4, S4, S4, D4, LAT,
                             mfa.Precision.BF16, k_buf=kb4, v_buf=vb4, stream=stream)
 
-        for _ in range(2):
-            step4()
+        warm(step4)
         barrier()
         t4 = time.perf_counter()
-        n4 = max(3, args.steps // 2)
+        n4 = 20
         for _ in range(n4):
             step4()
         barrier()
@@ -217,20 +231,7 @@ def main():
 
     # ------------------------------------------------- SURVEY §8(f) rows (one GPU's view)
     if not args.no_next:
-        def ev_time(fn, steps):
-            for _ in range(3):
-                fn()
-            torch.cuda.synchronize()
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(steps):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            return e0.elapsed_time(e1) / steps
-
-        nx = max(5, args.steps // 10)
+        nx = 20
         nxt = {}
         # Absorbed MLA at a decode shape: HBM-bound on the latent cache read.
         Bd, Hd, Sqd, Skd, Dd, LATd = 32, 16, 1, 4096, 128, 512
@@ -286,9 +287,11 @@ def main():
     def step():
         mha.forward(desc, q, k, v, o, l, stream=stream)
 
+    warm(step)  # untimed, time-based (the sections above may all be switched off)
     for _ in range(args.warmup):
         step()
     barrier()
+    mfa.last_launches()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -304,11 +307,12 @@ def main():
     value = total_flops / elapsed / 1e12
     achieved = flops_step / (kernel_ms * 1e-3) / 1e12
 
-    # The variant the library picks for this shape (mfa_api.cpp launch_forward ->
-    # attention_fwd_v2.hip fwd2_dispatch: causal with <= 768 row blocks runs the mirrored-pair
-    # kernel, otherwise one 128-row block per workgroup).
-    kname = ("mfa_fwd2_pair_kernel<F16, 128, 64, 4>" if (S + 127) // 128 * H * B <= 768
-             else "mfa_fwd2_kernel<F16, 128, 64, 2>")
+    # The kernel the library launched for this shape: the plan query (mfa_multihead_plan)
+    # names it, and the launch log of the timed calls must agree (one launch per step).
+    plan = mfa.multihead_plan(desc, mfa.KernelType.forward, Q=q, K=k, V=v, O=o, L=l)
+    ran = mfa.last_launches()
+    assert len(plan) == 1 and ran and all(r == plan[0] for r in ran), (plan, ran)
+    kname = plan[0]["name"]
     result = {
         "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
         "value": round(value, 2),
@@ -382,8 +386,10 @@ def cpu_baseline(S: int, D: int, H: int):
             "kind": "port",
             "sample": f"the full headline workload (B=1, H={H}, S={S}, D={D}, causal, fp32 "
                       f"inputs), oracle/mfa_oracle.c forward, {dt:.2f} s wall on {threads} "
-                      "threads; naive restatement of Network.swift (double accumulation; it "
-                      "computes the masked columns too, as the reference's CPU oracle does)"}
+                      "threads; naive restatement of Network.swift (double accumulation) with "
+                      "the reference CPU oracle's causal column limit colLimit = row + 1 "
+                      "(KernelRegressionTests.swift:92), so it computes exactly the "
+                      "S(S+1)/2 unmasked pairs it is credited with"}
 
 
 def cpu_next_rows(nxt: dict):

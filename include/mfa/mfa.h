@@ -252,6 +252,35 @@ mfa_status_t mfa_multihead_backward_key_value(const mfa_multihead_descriptor_t* 
                                               const mfa_attention_buffers_t* buffers,
                                               void* stream);
 
+/* Plan query: the kernels a call launches.  Runs the dispatcher of the call `type` names
+ * (FORWARD = mfa_multihead_forward, BACKWARD_QUERY / BACKWARD_KEY_VALUE = the two backward
+ * phases) with every launch recorded instead of issued, so the record is by construction
+ * what that call launches for these shapes, environment overrides and — when `buffers` is
+ * given — these pointers' alignment and strides (NULL: contiguous 256-byte aligned buffers).
+ * Nothing is read, written or allocated on the device; no GPU is needed.  Replaces the
+ * pipeline-state lookup of AttentionKernel / MultiHeadAttention.createPipeline
+ * (MultiHeadAttention.swift:386-430) as the place callers learn the kernel. */
+typedef struct mfa_kernel_launch {
+  char name[96];          /* kernel instantiation, e.g. "mfa_fwd2_pair_kernel<f16,D128,BK64,NWG2>" */
+  uint32_t threads;       /* workgroup size */
+  uint32_t lds_bytes;     /* dynamic LDS per workgroup */
+  uint64_t workgroups;    /* grid size */
+} mfa_kernel_launch_t;
+
+typedef struct mfa_kernel_plan {
+  int32_t count;          /* launches in issue order (0 for empty shapes) */
+  int32_t reserved;
+  mfa_kernel_launch_t launches[4];
+} mfa_kernel_plan_t;
+
+mfa_status_t mfa_multihead_plan(const mfa_multihead_descriptor_t* desc, mfa_kernel_type_t type,
+                                const mfa_attention_buffers_t* buffers, mfa_kernel_plan_t* out);
+
+/* The launches this host thread issued through the library since the previous call (the
+ * last four, in issue order, named like a plan), then clears the record.  Returns how many
+ * launches there were.  Lets a caller check that what ran is what the plan said. */
+int mfa_last_launches(mfa_kernel_plan_t* out);
+
 /* ---------------------------------------------------------------------------------- */
 /* Quantization (Sources/FlashAttention/GEMM/GEMMQuantization.swift).                  */
 
@@ -337,6 +366,15 @@ mfa_status_t mfa_quantized_backward_key_value(const mfa_quantized_descriptor_t* 
                                               const void* grad_output, const void* logsumexp,
                                               const void* d_values, float* grad_key,
                                               float* grad_value, void* stream);
+
+/* Plan query for the quantized calls (see mfa_multihead_plan): FORWARD =
+ * mfa_quantized_forward, BACKWARD_QUERY / BACKWARD_KEY_VALUE = the backward phases.  The
+ * tensors supply data pointers, scales and block layouts; NULL tensors plan per-tensor
+ * scale 1, zero point 0, aligned contiguous data. */
+mfa_status_t mfa_quantized_plan(const mfa_quantized_descriptor_t* desc, mfa_kernel_type_t type,
+                                const mfa_quantized_tensor_t* query,
+                                const mfa_quantized_tensor_t* key,
+                                const mfa_quantized_tensor_t* value, mfa_kernel_plan_t* out);
 
 /* GPU runtime quantization (GEMMQuantization.swift:305-623 semantics, bit-exact; the
  * reference does this on the CPU in QuantizedTensor.from, :720-860).

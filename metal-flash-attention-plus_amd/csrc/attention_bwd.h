@@ -381,15 +381,7 @@ hipError_t launch_bwd_q(const BwdParams& p, hipStream_t stream) {
   constexpr int TILEB = A::is_f32 ? BT * (DP + 1) * 4 : BT * DP * 2;
   constexpr int LDS = 4 * TILEB;
   auto kern = mfa_bwd_q_kernel<A, DP, BT, NW, KSRC>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.H), dim3(NW * 64), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(p.nblk * p.B * p.H), dim3(NW * 64), LDS, stream, p);
 }
 
 template <class A, int DP, int BT, int NW, int QSRC>
@@ -397,15 +389,7 @@ hipError_t launch_bwd_kv(const BwdParams& p, hipStream_t stream) {
   constexpr int TILEB = A::is_f32 ? BT * (DP + 1) * 4 : BT * DP * 2;
   constexpr int LDS = 4 * TILEB + 4 * BT * 4;
   auto kern = mfa_bwd_kv_kernel<A, DP, BT, NW, QSRC>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.Hkv), dim3(NW * 64), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(p.nblk * p.B * p.Hkv), dim3(NW * 64), LDS, stream, p);
 }
 
 }  // namespace mfa

@@ -675,17 +675,9 @@ static hipError_t launch_bwd_q_fast(const BwdParams& p, hipStream_t stream) {
   constexpr int BT = BwdFastCfg<DP>::BT;
   constexpr int LDS = 4 * BT * DP * 2;
   auto kern = mfa_bwd_q_fast_kernel<E, DP, BT>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
   BwdParams q = p;
   q.nblk = (p.R + 127) / 128;
-  hipLaunchKernelGGL(kern, dim3(q.nblk * p.B * p.H), dim3(256), LDS, stream, q);
-  return hipGetLastError();
+  return launch(kern, dim3(q.nblk * p.B * p.H), dim3(256), LDS, stream, q);
 }
 
 template <class E, int DP>
@@ -693,17 +685,9 @@ static hipError_t launch_bwd_kv_fast(const BwdParams& p, hipStream_t stream) {
   constexpr int BQ = BwdFastCfg<DP>::BQ;
   constexpr int LDS = 4 * BQ * DP * 2 + 4 * BQ * 4;
   auto kern = mfa_bwd_kv_fast_kernel<E, DP, BQ>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
   BwdParams q = p;
   q.nblk = (p.C + 127) / 128;
-  hipLaunchKernelGGL(kern, dim3(q.nblk * p.B * p.Hkv), dim3(256), LDS, stream, q);
-  return hipGetLastError();
+  return launch(kern, dim3(q.nblk * p.B * p.Hkv), dim3(256), LDS, stream, q);
 }
 
 // kind: 0 = backwardQuery, 1 = backwardKeyValue.  hipErrorNotSupported when not covered.

@@ -232,16 +232,8 @@ static hipError_t launch_fwd(const FwdParams& p, hipStream_t stream) {
   constexpr int TILEB = A::is_f32 ? BK * (DP + 1) * 4 : BK * DP * 2;
   constexpr int LDS = 4 * TILEB;
   auto kern = mfa_fwd_kernel<A, DP, BK, NW, KSRC, VSRC>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
   const int grid = p.nblk * p.B * p.H;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(grid), dim3(NW * 64), LDS, stream, p);
 }
 
 }  // namespace mfa

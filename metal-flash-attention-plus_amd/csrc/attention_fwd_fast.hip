@@ -485,31 +485,15 @@ static hipError_t launch_pair(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 8 * BK * DP * 2;  // two groups x (K, V) x double buffer
   static_assert(LDS >= 4 * (DP / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4, "merge area");
   auto kern = mfa_fwd_pair_kernel<E, DP, BK, KVSRC>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
   const int npairs = (p.nblk + 1) / 2;
-  hipLaunchKernelGGL(kern, dim3(npairs * p.B * p.H), dim3(512), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(npairs * p.B * p.H), dim3(512), LDS, stream, p);
 }
 
 template <class E, int DP, int BK, int KVSRC>
 static hipError_t launch_fast(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 4 * BK * DP * 2;
   auto kern = mfa_fwd_fast_kernel<E, DP, BK, KVSRC>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
 }
 
 // Returns hipErrorNotSupported when the configuration is not covered (caller falls back).

@@ -313,8 +313,7 @@ template <class E, int OCC>
 static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 2 * (64 * 128) + 2 * (128 * 64);
   auto kern = mfa_fwd_i8_kernel<E, 128, 64, OCC>;
-  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
 }
 
 // INT8-MFMA forward: Q fp16/bf16 (quantised per row in-kernel), K/V INT8 per-tensor with zero

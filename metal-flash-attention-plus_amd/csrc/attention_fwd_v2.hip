@@ -520,15 +520,7 @@ template <class E, int DP, int BK, int WPS, class TU = TuneDefault>
 static hipError_t launch_fwd2(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 4 * BK * DP * 2;
   auto kern = mfa_fwd2_kernel<E, DP, BK, WPS, TU>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
 }
 
 template <class E, int DP, int BK, int NWG>
@@ -537,18 +529,10 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
   static_assert(LDS >= NWG * (DP / 32) * 16 * 64 * 4 + NWG * 2 * 64 * 4, "merge area");
   static_assert(LDS >= NWG * 32 * (DP * 4 + 16), "O row image");
   auto kern = mfa_fwd2_pair_kernel<E, DP, BK, NWG>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
   FwdParams q = p;
   q.nblk = (p.R + NWG * 32 - 1) / (NWG * 32);
   const int npairs = (q.nblk + 1) / 2;
-  hipLaunchKernelGGL(kern, dim3(npairs * p.B * p.H), dim3(NWG * 128), LDS, stream, q);
-  return hipGetLastError();
+  return launch(kern, dim3(npairs * p.B * p.H), dim3(NWG * 128), LDS, stream, q);
 }
 
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).

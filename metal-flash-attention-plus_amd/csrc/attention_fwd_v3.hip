@@ -670,21 +670,6 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd3_kernel(FwdParams p) {
 
 }  // namespace fwd3
 
-// Per-device one-time kernel attribute (max dynamic LDS), safe under concurrent host threads.
-template <class K>
-static hipError_t set_lds_attr_once(K kern, int bytes) {
-  static std::once_flag flags[64];
-  static hipError_t errs[64];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::call_once(flags[dev & 63], [&] {
-    errs[dev & 63] = hipFuncSetAttribute((const void*)kern,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  });
-  return errs[dev & 63];
-}
-
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd3_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   if (DP != 128 || p.mask.window) return hipErrorNotSupported;
@@ -698,11 +683,8 @@ hipError_t fwd3_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   static const int tune = getenv("MFA_V3_TUNE") ? atoi(getenv("MFA_V3_TUNE")) : 0;
 #define MFA_F3T(EE, CA, T)                                                     \
   {                                                                            \
-    auto kern = fwd3::mfa_fwd3_kernel<EE, CA, T>;                              \
-    hipError_t e = set_lds_attr_once(kern, fwd3::LDS_BYTES);                   \
-    if (e != hipSuccess) return e;                                             \
-    hipLaunchKernelGGL(kern, grid, block, fwd3::LDS_BYTES, stream, q);         \
-    return hipGetLastError();                                                  \
+    return launch(fwd3::mfa_fwd3_kernel<EE, CA, T>, grid, block, fwd3::LDS_BYTES, \
+                  stream, q);                                    \
   }
 #define MFA_F3(EE, CA)                                                         \
   {                                                                            \

@@ -381,21 +381,11 @@ template <class E, int LAT>
 static hipError_t launch_latent(const LatentParams& p, hipStream_t stream) {
   constexpr int LDS = 2 * 32 * LAT * 2 + 4 * 64 * 16 * 4;
   auto kern = mfa_mla_latent_kernel<E, LAT>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(p.nblk * p.B * p.nsplit), dim3(256), LDS, stream, p);
-  if (p.nsplit > 1) {
-    // One row per workgroup measured fastest (B32 S_q 1: MNB 1/2/4 = 14.5/15.6/17.9 us): the
-    // W_v re-reads per batch item come from L2.
-    hipLaunchKernelGGL((mfa_mla_latent_merge_kernel<E, LAT, 1>), dim3(p.B * p.R), dim3(MNT), 0,
-                       stream, p);
-  }
-  return hipGetLastError();
+  hipError_t e = launch(kern, dim3(p.nblk * p.B * p.nsplit), dim3(256), LDS, stream, p);
+  if (e != hipSuccess || p.nsplit <= 1) return e;
+  // One row per workgroup measured fastest (B32 S_q 1: MNB 1/2/4 = 14.5/15.6/17.9 us): the
+  // W_v re-reads per batch item come from L2.
+  return launch(mfa_mla_latent_merge_kernel<E, LAT, 1>, dim3(p.B * p.R), dim3(MNT), 0, stream, p);
 }
 
 // Decode query projection Q̃[b, h, :] = q[b, h, :] · W_k[:, h·D : (h+1)·D]ᵀ (S_q = 1): a workgroup

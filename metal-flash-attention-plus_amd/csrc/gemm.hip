@@ -272,16 +272,8 @@ template <class E>
 static hipError_t launch_gemm2(const GemmParams& p, int batch, hipStream_t stream) {
   constexpr int LDS = 2 * (128 * 64 * 2) + 2 * (64 * 128 * 2);
   auto kern = mfa_gemm2_kernel<E>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
   const dim3 grid(p.N / 128, p.M / 128, batch);
-  hipLaunchKernelGGL(kern, grid, dim3(256), LDS, stream, p);
-  return hipGetLastError();
+  return launch(kern, grid, dim3(256), LDS, stream, p);
 }
 
 static bool gemm2_eligible(const GemmParams& p) {

@@ -18,6 +18,7 @@
 
 #include "../../include/mfa/mfa.h"
 #include "mfa_dispatch.h"
+#include "mfa_launch.h"
 #include "mfa_params.h"
 
 namespace {
@@ -128,6 +129,10 @@ int elem_of(int prec) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Stand-in device address for buffers a plan query does not have (never dereferenced: launches
+// are recorded, not issued).  256-byte aligned like any hipMalloc result.
+constexpr uintptr_t kPlanDummy = 0x100000;
 
 mfa::Operand make_operand(const void* ptr, int prec, int B, int Hx, int S, int D,
                           const int64_t* strides, int transposed) {
@@ -404,6 +409,41 @@ mfa_status_t mfa_attention_kernel_create(const mfa_kernel_descriptor_t* k,
                k->block_parallelization, k->block_traversal);
       break;
   }
+  // The kernel a call of this descriptor's shape (one batch item and head, R = C =
+  // sequence_length, dense, contiguous) launches: variant, workgroup size and LDS come from
+  // the plan query, so they name the instantiation that runs.
+  if (k->sequence_length > 0) {
+    mfa_multihead_descriptor_t md;
+    memset(&md, 0, sizeof(md));
+    mfa_attention_descriptor_init(&md.base);
+    const int qmem = k->memory_precisions[MFA_OPERAND_Q];
+    md.base.low_precision_inputs = qmem != MFA_PRECISION_FP32;
+    md.base.input_memory_precision = qmem;
+    md.base.low_precision_intermediates = k->memory_precisions[MFA_OPERAND_L] == MFA_PRECISION_FP16;
+    md.base.has_matrix_dimensions = 1;
+    md.base.row = md.base.column = k->sequence_length;
+    md.base.head = k->head_dimension;
+    md.base.has_transpose_state = 1;
+    md.base.transpose_q = k->transpose_state[MFA_OPERAND_Q];
+    md.base.transpose_k = k->transpose_state[MFA_OPERAND_K];
+    md.base.transpose_v = k->transpose_state[MFA_OPERAND_V];
+    md.base.transpose_o = k->transpose_state[MFA_OPERAND_O];
+    md.base.has_softmax_scale = 1;
+    md.base.softmax_scale = out->softmax_scale;
+    const mfa_multihead_shape_t sh = {1, 1, k->sequence_length, k->head_dimension, 0};
+    md.query_shape = md.key_shape = md.value_shape = sh;
+    md.broadcast_mode = MFA_BROADCAST_STANDARD;
+    const mfa_kernel_type_t t =
+        k->type == MFA_KERNEL_MLA_COMPRESSED ? MFA_KERNEL_FORWARD : (mfa_kernel_type_t)k->type;
+    mfa_kernel_plan_t plan;
+    const mfa_status_t st = mfa_multihead_plan(&md, t, nullptr, &plan);
+    if (st != MFA_SUCCESS) return st;
+    if (plan.count > 0) {
+      snprintf(out->variant, sizeof(out->variant), "%s", plan.launches[0].name);
+      out->threadgroup_size = (uint16_t)plan.launches[0].threads;
+      out->threadgroup_memory_allocation = plan.launches[0].lds_bytes;
+    }
+  }
   return MFA_SUCCESS;
 }
 
@@ -431,7 +471,12 @@ int mfa_multihead_broadcast_compatible(const mfa_multihead_descriptor_t* d) {
              k.sequence_length == s && v.sequence_length == s;
     }
     case MFA_BROADCAST_CUSTOM:
-      return 1;  // explicit shapes are taken as given
+      // The reference only compares the shapes with the ones the case carries
+      // (MultiHeadAttentionDescriptor.swift:97-106), which here are the descriptor's own; but the kernels still index K and V with one head count and one sequence length and
+      // map query head h to kv head h % Hkv: shapes they cannot address are rejected here
+      // rather than read out of bounds.
+      return same_b && same_d && k.num_heads == v.num_heads && k.num_heads > 0 &&
+             q.num_heads % k.num_heads == 0 && k.sequence_length == v.sequence_length;
     default:
       return 0;
   }
@@ -501,8 +546,8 @@ extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* 
   p.l_f16 = pl.pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
   void* L = buf->L;
   if (!L) {
-    st = scratch((size_t)pl.B * pl.H * pl.R * 4, &L, 0);
-    if (st != MFA_SUCCESS) return st;
+    if (mfa::plan_capture()) L = (void*)kPlanDummy;  // plan query: nothing is allocated
+    else if ((st = scratch((size_t)pl.B * pl.H * pl.R * 4, &L, 0)) != MFA_SUCCESS) return st;
   }
   p.l = L;
   p.B = pl.B; p.H = pl.H; p.Hkv = pl.Hkv; p.R = pl.R; p.C = pl.C; p.D = pl.D;
@@ -613,7 +658,8 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
   void* L = logsumexp;
   if (!L) {
-    if ((st = scratch((size_t)B * H * R * 4, &L, 0)) != MFA_SUCCESS) return st;
+    if (mfa::plan_capture()) L = (void*)kPlanDummy;  // plan query: nothing is allocated
+    else if ((st = scratch((size_t)B * H * R * 4, &L, 0)) != MFA_SUCCESS) return st;
   }
   p.l = L;
   p.B = B; p.H = H; p.Hkv = Hkv; p.R = R; p.C = C; p.D = D;
@@ -901,6 +947,122 @@ extern "C" mfa_status_t mfa_quantized_backward_key_value(
     float* grad_value, void* stream) {
   return quantized_backward(desc, query, key, value, nullptr, grad_output, logsumexp, nullptr,
                             grad_key, grad_value, (void*)d_values, PHASE_KV, stream);
+}
+
+// =========================================================================================
+// Plan query: the dispatchers above run with launches recorded (mfa_launch.h).
+namespace {
+
+struct CaptureScope {
+  mfa::PlanCapture cap;
+  mfa::PlanCapture* prev;
+  CaptureScope() : prev(mfa::plan_capture()) { mfa::plan_capture() = &cap; }
+  ~CaptureScope() { mfa::plan_capture() = prev; }
+  void copy_to(mfa_kernel_plan_t* out) const {
+    out->count = cap.count;
+    for (int i = 0; i < cap.count; ++i) {
+      static_assert(sizeof(out->launches[i].name) == sizeof(cap.rec[i].name), "name size");
+      memcpy(out->launches[i].name, cap.rec[i].name, sizeof(out->launches[i].name));
+      out->launches[i].threads = cap.rec[i].threads;
+      out->launches[i].lds_bytes = cap.rec[i].lds_bytes;
+      out->launches[i].workgroups = cap.rec[i].workgroups;
+    }
+  }
+};
+
+template <class T>
+void fill_dummy(T*& p) {
+  if (!p) p = (T*)kPlanDummy;
+}
+
+}  // namespace
+
+extern "C" mfa_status_t mfa_multihead_plan(const mfa_multihead_descriptor_t* desc,
+                                           mfa_kernel_type_t type,
+                                           const mfa_attention_buffers_t* buffers,
+                                           mfa_kernel_plan_t* out) {
+  if (!desc || !out) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  memset(out, 0, sizeof(*out));
+  mfa_attention_buffers_t b;
+  if (buffers) b = *buffers;
+  else memset(&b, 0, sizeof(b));
+  fill_dummy(b.Q); fill_dummy(b.K); fill_dummy(b.V); fill_dummy(b.O);
+  fill_dummy(b.D); fill_dummy(b.dO); fill_dummy(b.dV); fill_dummy(b.dK); fill_dummy(b.dQ);
+  if (type != MFA_KERNEL_FORWARD) fill_dummy(b.L);  // forward: NULL L plans the scratch case
+  if (desc->base.has_sparse_mask) fill_dummy(b.mask);
+  CaptureScope scope;
+  mfa_status_t st;
+  switch (type) {
+    case MFA_KERNEL_FORWARD: st = mfa_multihead_forward(desc, &b, nullptr); break;
+    case MFA_KERNEL_BACKWARD_QUERY: st = multihead_backward(desc, &b, nullptr, PHASE_QUERY); break;
+    case MFA_KERNEL_BACKWARD_KEY_VALUE: st = multihead_backward(desc, &b, nullptr, PHASE_KV); break;
+    default: return fail(MFA_ERR_UNSUPPORTED, "no multihead plan for kernel type %d", (int)type);
+  }
+  if (st == MFA_SUCCESS) scope.copy_to(out);
+  return st;
+}
+
+extern "C" int mfa_last_launches(mfa_kernel_plan_t* out) {
+  mfa::LaunchLog& log = mfa::launch_log();
+  const uint64_t n = std::min<uint64_t>(log.total, 4);
+  if (out) {
+    memset(out, 0, sizeof(*out));
+    out->count = (int32_t)n;
+    for (uint64_t j = 0; j < n; ++j) {
+      const int i = (int)((log.total - n + j) % mfa::LaunchLog::kMax);
+      mfa::kernel_symbol_name(log.handle[i], out->launches[j].name, sizeof(out->launches[j].name));
+      out->launches[j].threads = log.threads[i];
+      out->launches[j].lds_bytes = log.lds[i];
+      out->launches[j].workgroups = log.workgroups[i];
+    }
+  }
+  const int total = (int)std::min<uint64_t>(log.total, 1u << 30);
+  log.total = 0;
+  return total;
+}
+
+extern "C" mfa_status_t mfa_quantized_plan(const mfa_quantized_descriptor_t* desc,
+                                           mfa_kernel_type_t type,
+                                           const mfa_quantized_tensor_t* query,
+                                           const mfa_quantized_tensor_t* key,
+                                           const mfa_quantized_tensor_t* value,
+                                           mfa_kernel_plan_t* out) {
+  if (!desc || !out) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  memset(out, 0, sizeof(*out));
+  mfa_quantized_tensor_t t[3];
+  const mfa_quantized_tensor_t* in[3] = {query, key, value};
+  const int precs[3] = {desc->config.query_precision, desc->config.key_precision,
+                        desc->config.value_precision};
+  for (int i = 0; i < 3; ++i) {
+    if (in[i]) {
+      t[i] = *in[i];
+    } else {
+      memset(&t[i], 0, sizeof(t[i]));
+      t[i].precision = precs[i];
+      t[i].scale = 1.f;
+    }
+    fill_dummy(t[i].data);
+  }
+  float* const fd = (float*)kPlanDummy;
+  void* const vd = (void*)kPlanDummy;
+  CaptureScope scope;
+  mfa_status_t st;
+  switch (type) {
+    case MFA_KERNEL_FORWARD:
+      st = mfa_quantized_forward(desc, &t[0], &t[1], &t[2], fd, nullptr, nullptr, nullptr);
+      break;
+    case MFA_KERNEL_BACKWARD_QUERY:
+      st = quantized_backward(desc, &t[0], &t[1], &t[2], fd, vd, vd, fd, nullptr, nullptr, vd,
+                              PHASE_QUERY, nullptr);
+      break;
+    case MFA_KERNEL_BACKWARD_KEY_VALUE:
+      st = quantized_backward(desc, &t[0], &t[1], &t[2], nullptr, vd, vd, nullptr, fd, fd, vd,
+                              PHASE_KV, nullptr);
+      break;
+    default: return fail(MFA_ERR_UNSUPPORTED, "no quantized plan for kernel type %d", (int)type);
+  }
+  if (st == MFA_SUCCESS) scope.copy_to(out);
+  return st;
 }
 
 // =========================================================================================

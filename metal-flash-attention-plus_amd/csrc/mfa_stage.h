@@ -15,6 +15,7 @@
 #pragma once
 #include "mfa_device.h"
 #include "mfa_params.h"
+#include "mfa_launch.h"
 
 namespace mfa {
 

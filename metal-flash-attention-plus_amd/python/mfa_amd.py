@@ -192,6 +192,28 @@ class AttentionKernel(ctypes.Structure):
     ]
 
 
+class KernelLaunch(ctypes.Structure):
+    _fields_ = [
+        ("name", ctypes.c_char * 96),
+        ("threads", ctypes.c_uint32),
+        ("lds_bytes", ctypes.c_uint32),
+        ("workgroups", ctypes.c_uint64),
+    ]
+
+
+class KernelPlan(ctypes.Structure):
+    _fields_ = [
+        ("count", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("launches", KernelLaunch * 4),
+    ]
+
+    def as_list(self) -> list[dict]:
+        return [{"name": self.launches[i].name.decode(), "threads": self.launches[i].threads,
+                 "lds_bytes": self.launches[i].lds_bytes,
+                 "workgroups": self.launches[i].workgroups} for i in range(self.count)]
+
+
 class MultiHeadShape(ctypes.Structure):
     _fields_ = [
         ("batch_size", ctypes.c_uint32),
@@ -363,7 +385,13 @@ _sig("mfa_multihead_broadcast_compatible", ctypes.c_int, [_P(MultiHeadDescriptor
 for _n in ("mfa_multihead_forward", "mfa_multihead_backward", "mfa_multihead_backward_query",
            "mfa_multihead_backward_key_value"):
     _sig(_n, ctypes.c_int, [_P(MultiHeadDescriptor), _P(AttentionBuffers), _V])
+_sig("mfa_multihead_plan", ctypes.c_int,
+     [_P(MultiHeadDescriptor), ctypes.c_int, _P(AttentionBuffers), _P(KernelPlan)])
+_sig("mfa_last_launches", ctypes.c_int, [_P(KernelPlan)])
 _sig("mfa_quantized_configuration_init", None, [_P(QuantizedConfiguration)])
+_sig("mfa_quantized_plan", ctypes.c_int,
+     [_P(QuantizedDescriptor), ctypes.c_int, _P(QuantizedTensor), _P(QuantizedTensor),
+      _P(QuantizedTensor), _P(KernelPlan)])
 _sig("mfa_quantized_forward", ctypes.c_int,
      [_P(QuantizedDescriptor), _P(QuantizedTensor), _P(QuantizedTensor), _P(QuantizedTensor),
       _V, _V, _V, _V])
@@ -453,6 +481,37 @@ def make_buffers(**kw) -> tuple[AttentionBuffers, list]:
             setattr(b, name, s[0])
             keep.append(s[1])
     return b, keep
+
+
+def multihead_plan(desc: MultiHeadDescriptor, kind: KernelType = KernelType.forward,
+                   **buffers) -> list[dict]:
+    """Kernels the call `kind` launches for `desc` (and, if given, these tensors' pointers
+    and strides): [{name, threads, lds_bytes, workgroups}, ...] in issue order.  Needs no GPU."""
+    out = KernelPlan()
+    if buffers:
+        b, keep = make_buffers(**buffers)
+        bp = ctypes.byref(b)
+    else:
+        bp = None
+    check(lib.mfa_multihead_plan(ctypes.byref(desc), int(kind), bp, ctypes.byref(out)))
+    return out.as_list()
+
+
+def quantized_plan(desc: "QuantizedDescriptor", kind: KernelType = KernelType.forward,
+                   query=None, key=None, value=None) -> list[dict]:
+    """mfa_quantized_plan: the kernels a quantized call launches (see multihead_plan)."""
+    out = KernelPlan()
+    ref = lambda t: None if t is None else ctypes.byref(t)
+    check(lib.mfa_quantized_plan(ctypes.byref(desc), int(kind), ref(query), ref(key), ref(value),
+                                 ctypes.byref(out)))
+    return out.as_list()
+
+
+def last_launches() -> list[dict]:
+    """mfa_last_launches: the kernels this thread launched since the previous call."""
+    out = KernelPlan()
+    lib.mfa_last_launches(ctypes.byref(out))
+    return out.as_list()
 
 
 class MultiHeadAttention:

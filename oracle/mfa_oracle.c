@@ -181,7 +181,14 @@ static void score_row(const mfa_oracle_attention_args* a, int b, int h, int r, d
     lo = rp[0];
     hi = rp[1];
   }
+  /* Causal rows stop at colLimit = row + 1 (KernelRegressionTests.swift:92): the columns
+   * past it are masked whatever their score, so their dot products are not computed. */
+  const int climit = a->causal ? (r + 1 < a->C ? r + 1 : a->C) : a->C;
   for (int c = 0; c < a->C; ++c) {
+    if (c >= climit) {
+      x[c] = (double)kMaskValue;
+      continue;
+    }
     const float* k = kb + (int64_t)c * a->D;
     double dot = 0.0;
     for (int d = 0; d < a->D; ++d) dot += (double)q[d] * (double)k[d];

@@ -1,0 +1,143 @@
+"""CPU tests of the plan query (mfa_multihead_plan / mfa_quantized_plan): the dispatcher run
+with launches recorded, so no GPU is needed.  The GPU twin (test_plan_gpu.py) checks that the
+launches a real call issues are exactly these."""
+import ctypes
+
+import pytest
+
+import mfa_amd as mfa
+
+P = mfa.Precision
+K = mfa.KernelType
+
+
+def mh(B, H, S, D, causal=False, prec=P.FP16, C=None, Hkv=None):
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=prec, causal=causal)
+    return mfa.MultiHeadDescriptor.make(base, B, H, S, D, C=C, Hkv=Hkv)
+
+
+def one(plan):
+    assert len(plan) == 1, plan
+    return plan[0]
+
+
+# BASELINE.json configs: C2 (headline) fp16 causal H16 S4096 D128; C3 H16 S8192 non-causal;
+# C5 B8 H32 S4096 D256 fwd + bwd.
+def test_c2_headline_runs_mirrored_pair_kernel():
+    p = one(mfa.multihead_plan(mh(1, 16, 4096, 128, causal=True)))
+    assert p["name"] == "mfa_fwd2_pair_kernel<F16, 128, 64, 4>"
+    assert p["threads"] == 512 and p["lds_bytes"] == 128 * 1024
+    # 32 query blocks of 128 rows per head, mirrored in pairs: 16 x 16 heads.
+    assert p["workgroups"] == 16 * 16
+
+
+def test_c3_runs_single_block_kernel():
+    p = one(mfa.multihead_plan(mh(1, 16, 8192, 128)))
+    assert p["name"].startswith("mfa_fwd2_kernel<F16, 128, 64, 2")
+    assert p["threads"] == 256 and p["workgroups"] == 64 * 16
+
+
+def test_c5_forward_and_backward_phases():
+    d = mh(8, 32, 4096, 256)
+    f = one(mfa.multihead_plan(d))
+    assert f["name"].startswith("mfa_fwd2_kernel<F16, 256, 32, 2")
+    q = one(mfa.multihead_plan(d, K.backwardQuery))
+    kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
+    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32>"
+    assert kv["name"] == "mfa_bwd_kv_fast_kernel<F16, 256, 32>"
+    assert q["workgroups"] == 32 * 8 * 32 and kv["workgroups"] == 32 * 8 * 32
+    for r in (f, q, kv):
+        assert r["lds_bytes"] <= 160 * 1024
+
+
+def test_bf16_and_d64_instantiations():
+    assert one(mfa.multihead_plan(mh(1, 4, 1024, 128, prec=P.BF16)))["name"].startswith(
+        "mfa_fwd2_kernel<BF16, 128")
+    assert one(mfa.multihead_plan(mh(1, 16, 4096, 64, causal=True)))["name"] == \
+        "mfa_fwd2_pair_kernel<F16, 64, 64, 4>"
+
+
+def test_fp32_inputs_take_generic_kernel():
+    base = mfa.AttentionDescriptor.make(low_precision=False)
+    d = mfa.MultiHeadDescriptor.make(base, 1, 2, 256, 64)
+    assert one(mfa.multihead_plan(d))["name"].startswith("mfa_fwd_kernel<")
+
+
+def test_misaligned_query_falls_back_to_generic_kernel():
+    d = mh(1, 2, 256, 64)
+    b = mfa.AttentionBuffers()
+    b.Q, b.K, b.V, b.O = 0x100002, 0x200000, 0x300000, 0x400000  # Q off 16-byte alignment
+    out = mfa.KernelPlan()
+    mfa.check(mfa.lib.mfa_multihead_plan(ctypes.byref(d), 0, ctypes.byref(b), ctypes.byref(out)))
+    assert out.count == 1 and out.launches[0].name.startswith(b"mfa_fwd_kernel<")
+    b.Q = 0x100000
+    mfa.check(mfa.lib.mfa_multihead_plan(ctypes.byref(d), 0, ctypes.byref(b), ctypes.byref(out)))
+    assert out.launches[0].name.startswith(b"mfa_fwd2_")
+
+
+def test_quantized_plans():
+    base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
+    qi = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, integer_matmul=True)
+    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 64, 3>"
+    qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
+    assert one(mfa.quantized_plan(qx))["name"] == "mfa_fwd_fast_kernel<F16, 128, 64, 1>"
+    # Backward of quantized K/V runs the generic kernels with the INT8 source.
+    assert one(mfa.quantized_plan(qx, K.backwardQuery))["name"].startswith("mfa_bwd_q_kernel<")
+    # A non-zero zero point leaves the integer-matmul kernel.
+    zp = mfa.QuantizedTensor(None, int(P.INT8), 0.5, 3)
+    assert one(mfa.quantized_plan(qi, K.forward, None, zp, zp))["name"].startswith(
+        "mfa_fwd_fast_kernel<")
+
+
+def test_environment_override_is_visible_in_plan(monkeypatch):
+    d = mh(1, 16, 4096, 128, causal=True)
+    monkeypatch.setenv("MFA_FWD3", "1")
+    assert one(mfa.multihead_plan(d))["name"].startswith("fwd3::mfa_fwd3_kernel<F16, true")
+    monkeypatch.setenv("MFA_DISABLE_FAST", "1")
+    assert one(mfa.multihead_plan(d))["name"].startswith("mfa_fwd_kernel<")
+
+
+def test_attention_kernel_reports_dispatched_variant():
+    for causal, kind in ((True, K.forward), (False, K.backwardQuery), (False, K.backwardKeyValue)):
+        d = mfa.AttentionDescriptor.make(4096, 4096, 128, low_precision=True,
+                                         precision=P.FP16, causal=causal)
+        kern = mfa.attention_kernel(mfa.kernel_descriptor(d, kind))
+        md = mfa.MultiHeadDescriptor.make(
+            mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16), 1, 1, 4096, 128)
+        p = one(mfa.multihead_plan(md, kind))
+        assert kern.variant.decode() == p["name"]
+        assert kern.threadgroup_size == p["threads"]
+        assert kern.threadgroup_memory_allocation == p["lds_bytes"]
+
+
+def test_empty_shape_plans_nothing():
+    assert mfa.multihead_plan(mh(1, 2, 0, 64, C=64)) == []
+
+
+def test_invalid_descriptor_fails_like_the_call():
+    bad = mh(2, 8, 64, 32, Hkv=3)
+    bad.broadcast_mode = int(mfa.Broadcast.groupedQuery)
+    with pytest.raises(mfa.MFAError):
+        mfa.multihead_plan(bad)
+
+
+def test_no_launch_recorded_by_plan():
+    mfa.last_launches()
+    mfa.multihead_plan(mh(1, 16, 4096, 128, causal=True))
+    assert mfa.last_launches() == []
+
+
+@pytest.mark.parametrize("qh,kh,vh,kc,vc,ok", [
+    (8, 2, 2, 64, 64, True),    # GQA-shaped custom
+    (8, 3, 3, 64, 64, False),   # H % Hkv != 0
+    (8, 2, 4, 64, 64, False),   # K and V head counts differ
+    (8, 2, 2, 64, 32, False),   # K and V sequence lengths differ
+])
+def test_custom_broadcast_still_checks_addressable_shapes(qh, kh, vh, kc, vc, ok):
+    base = mfa.AttentionDescriptor.make()
+    d = mfa.MultiHeadDescriptor.make(base, 2, qh, 64, 32, Hkv=kh, C=kc, mode=mfa.Broadcast.custom)
+    d.value_shape = mfa.MultiHeadShape(2, vh, vc, 32, 0)
+    assert mfa.lib.mfa_multihead_broadcast_compatible(ctypes.byref(d)) == int(ok)
+    d2 = mfa.MultiHeadDescriptor.make(base, 2, qh, 64, 32, Hkv=kh, C=kc, mode=mfa.Broadcast.custom)
+    d2.key_shape = mfa.MultiHeadShape(3, kh, kc, 32, 0)  # batch mismatch
+    assert mfa.lib.mfa_multihead_broadcast_compatible(ctypes.byref(d2)) == 0

@@ -1,0 +1,128 @@
+"""GPU checks that the plan is the truth: for the BASELINE configurations the launches a real
+call issues (mfa_last_launches, recorded inside mfa::launch) are exactly the ones
+mfa_multihead_plan / mfa_quantized_plan return for the same descriptor and buffers; and that
+concurrent host threads driving the library on separate streams get bit-identical results
+(per-device, call_once kernel attributes)."""
+import threading
+
+import pytest
+import torch
+
+import mfa_amd as mfa
+
+pytestmark = pytest.mark.gpu
+P = mfa.Precision
+K = mfa.KernelType
+
+
+def mh(B, H, S, D, causal=False):
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16, causal=causal)
+    return mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+
+
+def tensors(B, H, S, D, dev, seed=0):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    q, k, v, do = ((torch.rand((B, H, S, D), generator=g, device=dev) - 0.5).half()
+                   for _ in range(4))
+    o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+    l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+    return q, k, v, do, o, l
+
+
+@pytest.mark.parametrize("B,H,S,D,causal", [
+    (1, 16, 4096, 128, True),    # C2 (headline)
+    (1, 16, 8192, 128, False),   # C3
+    (1, 32, 4096, 256, False),   # C5, one batch item
+    (2, 16, 4096, 64, True),
+])
+def test_forward_launches_match_plan(gpu, B, H, S, D, causal):
+    d = mh(B, H, S, D, causal)
+    q, k, v, _, o, l = tensors(B, H, S, D, gpu)
+    plan = mfa.multihead_plan(d, K.forward, Q=q, K=k, V=v, O=o, L=l)
+    mfa.last_launches()
+    mfa.MultiHeadAttention().forward(d, q, k, v, o, l)
+    torch.cuda.synchronize()
+    ran = mfa.last_launches()
+    assert ran == plan and len(plan) == 1
+    assert torch.isfinite(o).all()
+
+
+def test_backward_launches_match_plan(gpu):
+    B, H, S, D = 1, 32, 4096, 256  # C5 shape, one batch item
+    d = mh(B, H, S, D)
+    q, k, v, do, o, l = tensors(B, H, S, D, gpu)
+    dq, dk, dv = (torch.empty_like(o) for _ in range(3))
+    db = torch.empty((B, H, S), dtype=torch.bfloat16, device=gpu)
+    mha = mfa.MultiHeadAttention()
+    mha.forward(d, q, k, v, o, l)
+    bufs = dict(Q=q, K=k, V=v, O=o, L=l, dO=do, dQ=dq, dK=dk, dV=dv, D=db)
+    plan = (mfa.multihead_plan(d, K.backwardQuery, **bufs) +
+            mfa.multihead_plan(d, K.backwardKeyValue, **bufs))
+    mfa.last_launches()
+    mha.backward(d, q, k, v, o, do, l, dq, dk, dv, db)
+    torch.cuda.synchronize()
+    assert mfa.last_launches() == plan and len(plan) == 2
+
+
+@pytest.mark.parametrize("integer_matmul", [True, False])
+def test_int8_launches_match_plan(gpu, integer_matmul):
+    B, H, S, D = 1, 16, 8192, 128  # C3 INT8 leg
+    q = (torch.rand((B, H, S, D), device=gpu) - 0.5).half()
+    kq = torch.randint(-127, 128, (B, H, S, D), dtype=torch.int8, device=gpu)
+    vq = torch.randint(-127, 128, (B, H, S, D), dtype=torch.int8, device=gpu)
+    o = torch.empty((B, H, S, D), dtype=torch.float32, device=gpu)
+    l = torch.empty((B, H, S), dtype=torch.float16, device=gpu)
+    base = mfa.AttentionDescriptor.make(S, S, D, low_precision=True, precision=P.FP16)
+    desc = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=B, H=H,
+                                    integer_matmul=integer_matmul)
+    tq = mfa.quantized_tensor(q, P.FP16)
+    tk = mfa.quantized_tensor(kq, P.INT8, scale=0.01)
+    tv = mfa.quantized_tensor(vq, P.INT8, scale=0.01)
+    plan = mfa.quantized_plan(desc, K.forward, tq, tk, tv)
+    mfa.last_launches()
+    mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+    torch.cuda.synchronize()
+    assert mfa.last_launches() == plan and len(plan) == 1
+    want = "mfa_fwd_i8_kernel<" if integer_matmul else "mfa_fwd_fast_kernel<"
+    assert plan[0]["name"].startswith(want)
+
+
+@pytest.mark.parametrize("D,causal", [(128, True), (256, False)])
+def test_two_host_threads_bit_identical(gpu, D, causal):
+    """Two host threads, each on its own stream, run the forward concurrently; each result
+    equals the single-threaded result bit for bit."""
+    B, H, S = 1, 8, 2048
+    d = mh(B, H, S, D, causal)
+    ins = [tensors(B, H, S, D, gpu, seed=s) for s in (1, 2)]
+    mha = mfa.MultiHeadAttention()
+    ref = []
+    for q, k, v, _, o, l in ins:
+        mha.forward(d, q, k, v, o, l)
+        torch.cuda.synchronize()
+        ref.append((o.clone(), l.clone()))
+        o.zero_()
+        l.zero_()
+    errors = []
+
+    def worker(i):
+        try:
+            torch.cuda.set_device(gpu)
+            s = torch.cuda.Stream(device=gpu)
+            q, k, v, _, o, l = ins[i]
+            for _ in range(20):
+                mha.forward(d, q, k, v, o, l, stream=s.cuda_stream)
+            s.synchronize()
+        except Exception as e:  # reported below
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
+    for (q, k, v, _, o, l), (o_ref, l_ref) in zip(ins, ref):
+        assert torch.equal(o, o_ref)
+        assert torch.equal(l, l_ref)
