@@ -367,6 +367,44 @@ mfa_status_t mfa_quantized_backward_key_value(const mfa_quantized_descriptor_t* 
                                               const void* d_values, float* grad_key,
                                               float* grad_value, void* stream);
 
+/* QuantizedKernelLayoutManifest (Attention/QuantizedKernelLayoutManifest.swift:8-266): the
+ * buffer slot of every quantized-attention operand per kernel type, the reference FFI's
+ * binding contract.  Keys in declaration order (Key, :16-56). */
+typedef enum mfa_quantized_slot_key {
+  MFA_QSLOT_Q_DATA = 0, MFA_QSLOT_K_DATA, MFA_QSLOT_V_DATA, MFA_QSLOT_OUTPUT,
+  MFA_QSLOT_GRAD_OUTPUT, MFA_QSLOT_LOGSUMEXP, MFA_QSLOT_GRAD_QUERY, MFA_QSLOT_D_VALUES,
+  MFA_QSLOT_GRAD_KEY, MFA_QSLOT_GRAD_VALUE, MFA_QSLOT_Q_SCALE, MFA_QSLOT_Q_ZERO_POINT,
+  MFA_QSLOT_K_SCALE, MFA_QSLOT_K_ZERO_POINT, MFA_QSLOT_V_SCALE, MFA_QSLOT_V_ZERO_POINT,
+  MFA_QSLOT_DIMS, MFA_QSLOT_STE_CLIP_RANGE, MFA_QSLOT_Q_BLOCK_SCALES,
+  MFA_QSLOT_Q_BLOCK_ZERO_POINTS, MFA_QSLOT_K_BLOCK_SCALES, MFA_QSLOT_K_BLOCK_ZERO_POINTS,
+  MFA_QSLOT_V_BLOCK_SCALES, MFA_QSLOT_V_BLOCK_ZERO_POINTS, MFA_QSLOT_Q_PRECOMPUTED_SUMS,
+  MFA_QSLOT_K_PRECOMPUTED_SUMS, MFA_QSLOT_V_PRECOMPUTED_SUMS, MFA_QSLOT_Q_STRIDES,
+  MFA_QSLOT_K_STRIDES, MFA_QSLOT_V_STRIDES, MFA_QSLOT_O_STRIDES, MFA_QSLOT_MASK_BUFFER,
+  MFA_QSLOT_MASK_METADATA, MFA_QSLOT_NUM_HEADS, MFA_QSLOT_NUM_KEY_VALUE_HEADS,
+  MFA_QSLOT_HEAD_DIMENSION, MFA_QSLOT_SEQUENCE_LENGTH, MFA_QSLOT_SCRATCH0, MFA_QSLOT_SCRATCH1,
+  MFA_QSLOT_COUNT
+} mfa_quantized_slot_key_t;
+
+/* Layout.index(key) of QuantizedKernelLayoutManifest.layout(for: kernel): the slot, or -1
+ * when that kernel's layout does not bind the key. */
+int mfa_quantized_slot(mfa_kernel_type_t kernel, mfa_quantized_slot_key_t key);
+/* The whole layout: out[key] = mfa_quantized_slot(kernel, key) for key < min(n,
+ * MFA_QSLOT_COUNT).  Returns how many keys have a slot, or -1 for an unknown kernel. */
+int mfa_quantized_slot_table(mfa_kernel_type_t kernel, int32_t* out, int n);
+/* Key.rawValue ("qData", ..., "scratch1"), NULL when out of range. */
+const char* mfa_quantized_slot_name(mfa_quantized_slot_key_t key);
+
+/* GLUON constants (AttentionKernel+GluonOptimizations.swift:12-22) and the predicate that
+ * gates the GLUON softmax (:314-320, block traversal >= 512 and block head >= 64).  No
+ * parameter table produces such a block, here or in the reference, so the standard
+ * softmax always runs. */
+#define MFA_GLUON_SPLIT_EXP_FACTOR 4
+#define MFA_GLUON_CHANNEL_SYNC_POINTS 2
+#define MFA_GLUON_SUBTILE_SIZE 16
+void mfa_gluon_constants(uint8_t* split_exp_factor, uint8_t* channel_sync_points,
+                         uint8_t* subtile_size);
+int mfa_gluon_should_enable(uint16_t block_traversal, uint16_t block_head);
+
 /* Plan query for the quantized calls (see mfa_multihead_plan): FORWARD =
  * mfa_quantized_forward, BACKWARD_QUERY / BACKWARD_KEY_VALUE = the backward phases.  The
  * tensors supply data pointers, scales and block layouts; NULL tensors plan per-tensor

@@ -388,6 +388,11 @@ for _n in ("mfa_multihead_forward", "mfa_multihead_backward", "mfa_multihead_bac
 _sig("mfa_multihead_plan", ctypes.c_int,
      [_P(MultiHeadDescriptor), ctypes.c_int, _P(AttentionBuffers), _P(KernelPlan)])
 _sig("mfa_last_launches", ctypes.c_int, [_P(KernelPlan)])
+_sig("mfa_quantized_slot", ctypes.c_int, [ctypes.c_int, ctypes.c_int])
+_sig("mfa_quantized_slot_table", ctypes.c_int, [ctypes.c_int, _P(ctypes.c_int32), ctypes.c_int])
+_sig("mfa_quantized_slot_name", ctypes.c_char_p, [ctypes.c_int])
+_sig("mfa_gluon_constants", None, [_P(ctypes.c_uint8)] * 3)
+_sig("mfa_gluon_should_enable", ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint16])
 _sig("mfa_quantized_configuration_init", None, [_P(QuantizedConfiguration)])
 _sig("mfa_quantized_plan", ctypes.c_int,
      [_P(QuantizedDescriptor), ctypes.c_int, _P(QuantizedTensor), _P(QuantizedTensor),
@@ -505,6 +510,25 @@ def quantized_plan(desc: "QuantizedDescriptor", kind: KernelType = KernelType.fo
     check(lib.mfa_quantized_plan(ctypes.byref(desc), int(kind), ref(query), ref(key), ref(value),
                                  ctypes.byref(out)))
     return out.as_list()
+
+
+QSLOT_COUNT = 39
+
+
+def quantized_layout(kind: KernelType) -> dict[str, int]:
+    """QuantizedKernelLayoutManifest.layout(for:).dictionary(): key name -> slot (-1 = the
+    layout lists the key but gives it no slot); keys the layout does not list are absent."""
+    out = (ctypes.c_int32 * QSLOT_COUNT)()
+    if lib.mfa_quantized_slot_table(int(kind), out, QSLOT_COUNT) < 0:
+        raise ValueError(kind)
+    return {lib.mfa_quantized_slot_name(k).decode(): out[k] for k in range(QSLOT_COUNT)}
+
+
+def gluon_constants() -> tuple[int, int, int]:
+    """(SPLIT_EXP_FACTOR, CHANNEL_SYNC_POINTS, SUBTILE_SIZE)."""
+    v = [ctypes.c_uint8() for _ in range(3)]
+    lib.mfa_gluon_constants(*[ctypes.byref(x) for x in v])
+    return tuple(x.value for x in v)
 
 
 def last_launches() -> list[dict]:
