@@ -504,8 +504,10 @@ mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const void* kv_la
  * K/V — Q̃_h = Q_h·W_k,hᵀ, Õ_h = softmax(scale·Q̃_h·latentᵀ)·latent, O_h = Õ_h·W_v,h — with
  * scale = softmax_scale of the base descriptor or 1/sqrt(head_dim).  Same arguments and
  * layouts as mfa_mla_forward; kv_latent_dim must be 256 or 512; masks: none or causal.
- * `workspace` (nullable → library-owned) holds Q̃ and Õ:
- * mfa_mla_absorbed_workspace_size() bytes. */
+ * `workspace` (nullable → library-owned) holds Q̃, Õ and, for decode shapes, the split-KV
+ * partials: mfa_mla_absorbed_workspace_size() bytes.  Library-owned buffers (here, the
+ * decompressed K/V of mfa_mla_forward and a forward's NULL L) are kept per device and per
+ * stream, so concurrent calls on different streams never share one. */
 size_t mfa_mla_absorbed_workspace_size(const mfa_mla_descriptor_t* desc);
 mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* desc, const void* kv_latent,
                                       const void* w_k, const void* w_v, const void* query,

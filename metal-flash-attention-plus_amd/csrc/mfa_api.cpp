@@ -13,6 +13,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -60,30 +61,40 @@ int pad_head(int D) {
   return -1;
 }
 
-// Library-owned scratch (L when the caller passes none: MultiHeadAttention.swift:296-319
-// allocates and zero-fills one per call).  One buffer per device, grown on demand.
+// Library-owned scratch for buffers the caller does not pass (L in forward:
+// MultiHeadAttention.swift:296-319 allocates one per call; MLA's decompressed K/V, Q~/O~ and
+// split-KV partials).  One buffer per (device, stream, use): calls on different streams never
+// share one.  Growth is stream-ordered (hipFreeAsync + hipMallocAsync on the call's stream),
+// so the old buffer is released only after the work queued before it on that stream.
+struct ScratchKey {
+  int dev;
+  hipStream_t stream;
+  int slot;
+  bool operator<(const ScratchKey& o) const {
+    if (dev != o.dev) return dev < o.dev;
+    if (stream != o.stream) return (uintptr_t)stream < (uintptr_t)o.stream;
+    return slot < o.slot;
+  }
+};
 struct Scratch {
   std::mutex mu;
-  void* ptr[64] = {};
-  size_t bytes[64] = {};
+  std::map<ScratchKey, std::pair<void*, size_t>> bufs;
 } g_scratch;
 
-mfa_status_t scratch(size_t bytes, void** out, int slot_hint = 0) {
+mfa_status_t scratch(size_t bytes, void** out, int slot, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(MFA_ERR_NO_DEVICE, "no HIP device");
-  const int slot = (dev * 4 + slot_hint) % 64;
   std::lock_guard<std::mutex> lock(g_scratch.mu);
-  if (g_scratch.bytes[slot] < bytes) {
-    if (g_scratch.ptr[slot]) (void)hipFree(g_scratch.ptr[slot]);
-    g_scratch.ptr[slot] = nullptr;
-    g_scratch.bytes[slot] = 0;
+  auto& b = g_scratch.bufs[ScratchKey{dev, stream, slot}];
+  if (b.second < bytes) {
+    if (b.first) (void)hipFreeAsync(b.first, stream);
+    b = {nullptr, 0};
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e != hipSuccess) return hip_status(e, "hipMalloc(scratch)");
-    g_scratch.ptr[slot] = p;
-    g_scratch.bytes[slot] = bytes;
+    hipError_t e = hipMallocAsync(&p, bytes, stream);
+    if (e != hipSuccess) return hip_status(e, "hipMallocAsync(scratch)");
+    b = {p, bytes};
   }
-  *out = g_scratch.ptr[slot];
+  *out = b.first;
   return MFA_SUCCESS;
 }
 
@@ -260,6 +271,21 @@ hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, 
   return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
 }
 
+// Transposed layouts the kernels honour: Q, K and V of the multi-head forward (column-major
+// within a head, AttentionKernelDescriptor.swift:34-47).  A transposed O (forward output,
+// backward input and dO) and the transposed gradients the reference writes when Q/K/V are
+// transposed are not implemented: those calls fail instead of writing a dense layout the
+// caller did not ask for.  `qkv_ok` = the call honours transposed Q/K/V.
+mfa_status_t check_transposes(const mfa_attention_descriptor_t& d, bool qkv_ok, const char* what) {
+  if (!d.has_transpose_state) return MFA_SUCCESS;
+  if (d.transpose_o)
+    return fail(MFA_ERR_UNSUPPORTED, "%s: transposed O / dO is not supported", what);
+  if (!qkv_ok && (d.transpose_q || d.transpose_k || d.transpose_v))
+    return fail(MFA_ERR_UNSUPPORTED, "%s: transposed Q/K/V (and gradients) are not supported",
+                what);
+  return MFA_SUCCESS;
+}
+
 float resolve_scale(const mfa_attention_descriptor_t& d, int head_dim) {
   // AttentionKernel.swift:63-68: default 1/sqrt(head_dim).
   if (d.has_softmax_scale) return d.softmax_scale;
@@ -321,6 +347,11 @@ mfa_status_t mfa_attention_kernel_descriptor(const mfa_attention_descriptor_t* d
   if (!desc->has_matrix_dimensions || !desc->has_transpose_state)
     return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
   memset(out, 0, sizeof(*out));
+  {
+    const bool fwd = type == MFA_KERNEL_FORWARD;
+    const mfa_status_t st = check_transposes(*desc, fwd, fwd ? "forward kernel" : "kernel");
+    if (st != MFA_SUCCESS) return st;
+  }
   const Precisions pr = resolve_precisions(*desc);
   const int D = desc->head;
   const int DP = pad_head(D);
@@ -530,6 +561,7 @@ extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* 
   MHAPlan pl;
   mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
   if (st != MFA_SUCCESS) return st;
+  if ((st = check_transposes(desc->base, true, "forward")) != MFA_SUCCESS) return st;
   if (pl.R == 0) return MFA_SUCCESS;
   const mfa_attention_descriptor_t& base = desc->base;
   const int prec = pl.pr.mem[MFA_OPERAND_Q];
@@ -547,7 +579,8 @@ extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* 
   void* L = buf->L;
   if (!L) {
     if (mfa::plan_capture()) L = (void*)kPlanDummy;  // plan query: nothing is allocated
-    else if ((st = scratch((size_t)pl.B * pl.H * pl.R * 4, &L, 0)) != MFA_SUCCESS) return st;
+    else if ((st = scratch((size_t)pl.B * pl.H * pl.R * 4, &L, 0, (hipStream_t)stream)) != MFA_SUCCESS)
+      return st;
   }
   p.l = L;
   p.B = pl.B; p.H = pl.H; p.Hkv = pl.Hkv; p.R = pl.R; p.C = pl.C; p.D = pl.D;
@@ -628,6 +661,8 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
   const int DP = pad_head(D);
   if (DP < 0 || D <= 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d", D);
+  mfa_status_t st0 = check_transposes(base, false, "quantized forward");
+  if (st0 != MFA_SUCCESS) return st0;
   const mfa_quantized_configuration_t& cfg = desc->config;
   const int qp = cfg.query_precision, kp = cfg.key_precision, vp = cfg.value_precision;
   // Compute element type: the floating-point input type, FP16 when every input is integer.
@@ -659,7 +694,8 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   void* L = logsumexp;
   if (!L) {
     if (mfa::plan_capture()) L = (void*)kPlanDummy;  // plan query: nothing is allocated
-    else if ((st = scratch((size_t)B * H * R * 4, &L, 0)) != MFA_SUCCESS) return st;
+    else if ((st = scratch((size_t)B * H * R * 4, &L, 0, (hipStream_t)stream)) != MFA_SUCCESS)
+      return st;
   }
   p.l = L;
   p.B = B; p.H = H; p.Hkv = Hkv; p.R = R; p.C = C; p.D = D;
@@ -808,6 +844,7 @@ mfa_status_t multihead_backward(const mfa_multihead_descriptor_t* desc,
   MHAPlan pl;
   mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
   if (st != MFA_SUCCESS) return st;
+  if ((st = check_transposes(desc->base, false, "backward")) != MFA_SUCCESS) return st;
   const mfa_attention_descriptor_t& base = desc->base;
   const int prec = pl.pr.mem[MFA_OPERAND_Q];
   mfa::BwdParams p;
@@ -879,6 +916,8 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
   const int DP = pad_head(D);
   if (DP < 0 || D <= 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d", D);
+  mfa_status_t st0 = check_transposes(base, false, "quantized backward");
+  if (st0 != MFA_SUCCESS) return st0;
   const mfa_quantized_configuration_t& cfg = desc->config;
   const int qp = cfg.query_precision, kp = cfg.key_precision, vp = cfg.value_precision;
   int elem = -1;
@@ -1084,14 +1123,19 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
   if (B <= 0 || H <= 0 || D <= 0 || Lat <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "empty MLA shape");
   const int DP = pad_head(D);
   if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", D);
+  mfa_status_t st0 = check_transposes(desc->base, false, "MLA forward");
+  if (st0 != MFA_SUCCESS) return st0;
   const int64_t kv_elems = (int64_t)B * Skv * H * D;
   hipStream_t s = (hipStream_t)stream;
   mfa_status_t st;
   void* kb = decompressed_k;
   void* vb = decompressed_v;
-  if (!kb || !vb) {
+  if (!kb != !vb)
+    return fail(MFA_ERR_INVALID_ARGUMENT,
+                "MLA forward: pass both decompressed K and V buffers, or neither");
+  if (!kb) {
     void* both = nullptr;
-    if ((st = scratch((size_t)kv_elems * 2 * 2, &both, 1)) != MFA_SUCCESS) return st;
+    if ((st = scratch((size_t)kv_elems * 2 * 2, &both, 1, s)) != MFA_SUCCESS) return st;
     kb = both;
     vb = (char*)both + kv_elems * 2;
   }
@@ -1122,7 +1166,7 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
   p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
   void* L = logsumexp;
   if (!L) {
-    if ((st = scratch((size_t)B * H * Sq * 4, &L, 0)) != MFA_SUCCESS) return st;
+    if ((st = scratch((size_t)B * H * Sq * 4, &L, 0, s)) != MFA_SUCCESS) return st;
   }
   p.l = L;
   p.B = B; p.H = H; p.Hkv = H; p.R = Sq; p.C = Skv; p.D = D;
@@ -1142,10 +1186,46 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
 // (attention_mla_latent.hip), O = Õ·W_v per head (16-bit GEMM).  Same result as
 // mfa_mla_forward up to the rounding of Q̃ and Õ to the 16-bit precision (where the
 // decompress path rounds K and V).
+namespace {
+
+// Key split of the latent attention: when the query blocks alone cannot fill the chip
+// (decode shapes), aim at >= 512 workgroups, each split at least 4 tiles of 32 keys.
+struct AbsorbedLayout {
+  int nblk, nsplit, chunk;
+  size_t qt_bytes;     // Q~ and O~, 16-bit, each
+  size_t part_bytes;   // split-KV partial O (FP32) + (m, l) pairs, 0 without a split
+  size_t total() const { return 2 * ((qt_bytes + 255) & ~(size_t)255) + part_bytes; }
+};
+
+AbsorbedLayout absorbed_layout(int B, int H, int Sq, int Skv, int Lat) {
+  AbsorbedLayout a;
+  const int R = H * Sq;
+  a.nblk = (R + 31) / 32;
+  a.nsplit = 1;
+  a.chunk = Skv;
+  const int blocks = a.nblk * B;
+  const int tiles = (Skv + 31) / 32;
+  int ns = (512 + blocks - 1) / blocks;
+  ns = std::min(ns, std::max(1, tiles / 4));
+  if (ns > 1) {
+    const int per = (tiles + ns - 1) / ns;  // tiles per split
+    a.chunk = per * 32;
+    a.nsplit = (tiles + per - 1) / per;
+  }
+  a.qt_bytes = (size_t)B * R * Lat * 2;
+  a.part_bytes = a.nsplit > 1 ? (size_t)B * a.nsplit * R * Lat * 4 + (size_t)B * a.nsplit * R * 8
+                              : 0;
+  return a;
+}
+
+}  // namespace
+
 extern "C" size_t mfa_mla_absorbed_workspace_size(const mfa_mla_descriptor_t* desc) {
   if (!desc) return 0;
-  return (size_t)2 * desc->batch_size * desc->num_heads * desc->sequence_length_q *
-         desc->kv_latent_dim * 2;
+  return absorbed_layout((int)desc->batch_size, (int)desc->num_heads,
+                         (int)desc->sequence_length_q, (int)desc->sequence_length_kv,
+                         (int)desc->kv_latent_dim)
+      .total();
 }
 
 extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* desc,
@@ -1167,14 +1247,19 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
   const int sp = desc->base.sparsity_pattern;
   if (sp != MFA_SPARSITY_NONE && sp != MFA_SPARSITY_CAUSAL)
     return fail(MFA_ERR_UNSUPPORTED, "absorbed MLA supports no mask or causal");
+  mfa_status_t st0 = check_transposes(desc->base, false, "absorbed MLA forward");
+  if (st0 != MFA_SUCCESS) return st0;
   if (Sq == 0) return MFA_SUCCESS;
   hipStream_t s = (hipStream_t)stream;
   mfa_status_t st;
-  const int64_t qlat = (int64_t)B * H * Sq * Lat;  // elements of Q̃ (and of Õ)
+  // Q~, O~ and the split-KV partials, carved from the caller's workspace
+  // (mfa_mla_absorbed_workspace_size bytes) or from this stream's scratch.
+  const AbsorbedLayout al = absorbed_layout(B, H, Sq, Skv, Lat);
   void* ws = workspace;
-  if (!ws && (st = scratch((size_t)qlat * 2 * 2, &ws, 2)) != MFA_SUCCESS) return st;
+  if (!ws && (st = scratch(al.total(), &ws, 2, s)) != MFA_SUCCESS) return st;
   char* qt = (char*)ws;
-  char* ot = qt + qlat * 2;
+  char* ot = qt + ((al.qt_bytes + 255) & ~(size_t)255);
+  char* part = ot + ((al.qt_bytes + 255) & ~(size_t)255);
   // One launch per GEMM over all (b, h): W_k / W_v slices depend on h only (bmod = H).
   auto general = [&](const void* a, const void* w, void* c, int M, int N, int K, int lda,
                      int ldc, int trans_b, int prec_c, int64_t sa, int64_t sc, int nbatch,
@@ -1229,31 +1314,15 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
   lp.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
   lp.l = logsumexp;
   lp.B = B; lp.R = H * Sq; lp.Sq = Sq; lp.Skv = Skv;
-  lp.nblk = (lp.R + 31) / 32;
+  lp.nblk = al.nblk;
   lp.c_log2 = 1.442695041f * resolve_scale(desc->base, D);
   lp.causal = sp == MFA_SPARSITY_CAUSAL;
-  // Split the keys when the query blocks alone cannot fill the chip (decode shapes): aim at
-  // >= 512 workgroups, each split at least 4 tiles of 32 keys.
-  lp.nsplit = 1;
-  lp.chunk = Skv;
-  {
-    const int blocks = lp.nblk * B;
-    const int tiles = (Skv + 31) / 32;
-    int ns = (512 + blocks - 1) / blocks;
-    ns = std::min(ns, std::max(1, tiles / 4));
-    if (ns > 1) {
-      const int per = (tiles + ns - 1) / ns;   // tiles per split
-      lp.chunk = per * 32;
-      lp.nsplit = (tiles + per - 1) / per;
-    }
-  }
+  lp.nsplit = al.nsplit;
+  lp.chunk = al.chunk;
   if (lp.nsplit > 1) {
     const size_t obytes = (size_t)B * lp.nsplit * lp.R * Lat * 4;
-    const size_t mbytes = (size_t)B * lp.nsplit * lp.R * 8;
-    void* part = nullptr;
-    if ((st = scratch(obytes + mbytes, &part, 3)) != MFA_SUCCESS) return st;
     lp.opart = (float*)part;
-    lp.mlpart = (float2*)((char*)part + obytes);
+    lp.mlpart = (float2*)(part + obytes);
     // The merge pass applies W_v itself (FP32 Õ, one launch fewer).
     lp.wv = w_v;
     lp.out = output;

@@ -141,3 +141,78 @@ def test_custom_broadcast_still_checks_addressable_shapes(qh, kh, vh, kc, vc, ok
     d2 = mfa.MultiHeadDescriptor.make(base, 2, qh, 64, 32, Hkv=kh, C=kc, mode=mfa.Broadcast.custom)
     d2.key_shape = mfa.MultiHeadShape(3, kh, kc, 32, 0)  # batch mismatch
     assert mfa.lib.mfa_multihead_broadcast_compatible(ctypes.byref(d2)) == 0
+
+
+def test_custom_mismatch_rejected_by_the_call():
+    base = mfa.AttentionDescriptor.make()
+    d = mfa.MultiHeadDescriptor.make(base, 2, 8, 64, 32, Hkv=2, mode=mfa.Broadcast.custom)
+    d.value_shape = mfa.MultiHeadShape(2, 2, 48, 32, 0)  # V shorter than K
+    b = mfa.AttentionBuffers()
+    b.Q = b.K = b.V = b.O = 0x100000  # never dereferenced: validation fails first
+    assert mfa.lib.mfa_multihead_forward(ctypes.byref(d), ctypes.byref(b), None) == 1
+    with pytest.raises(mfa.MFAError):
+        mfa.multihead_plan(d)
+
+
+# transposed O and transposed gradients are rejected, not silently written dense.
+def test_transposed_o_rejected():
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16,
+                                        transpose=(False, False, False, True))
+    d = mfa.MultiHeadDescriptor.make(base, 1, 2, 128, 64)
+    for kind in (K.forward, K.backwardQuery, K.backwardKeyValue):
+        with pytest.raises(mfa.MFAError) as e:
+            mfa.multihead_plan(d, kind)
+        assert e.value.status == 2
+
+
+def test_transposed_qkv_forward_only():
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16,
+                                        transpose=(True, True, True, False))
+    d = mfa.MultiHeadDescriptor.make(base, 1, 2, 128, 64)
+    assert one(mfa.multihead_plan(d))["name"].startswith("mfa_fwd_kernel<")  # strided operands
+    for kind in (K.backwardQuery, K.backwardKeyValue):
+        with pytest.raises(mfa.MFAError) as e:
+            mfa.multihead_plan(d, kind)
+        assert e.value.status == 2
+    full = mfa.AttentionDescriptor.make(128, 128, 64, transpose=(True, False, False, False))
+    mfa.kernel_descriptor(full, K.forward)
+    with pytest.raises(mfa.MFAError):
+        mfa.kernel_descriptor(full, K.backwardQuery)
+
+
+def test_quantized_rejects_transposes():
+    base = mfa.AttentionDescriptor.make(256, 256, 128, low_precision=True, precision=P.FP16,
+                                        transpose=(False, True, False, False))
+    qd = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=2)
+    with pytest.raises(mfa.MFAError) as e:
+        mfa.quantized_plan(qd)
+    assert e.value.status == 2
+
+
+def mla_desc(B, H, Sq, Skv, D, Lat):
+    d = mfa.MLADescriptor()
+    d.base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.BF16)
+    d.batch_size, d.num_heads = B, H
+    d.sequence_length_q, d.sequence_length_kv = Sq, Skv
+    d.head_dim, d.kv_latent_dim = D, Lat
+    d.precision = int(P.BF16)
+    return d
+
+
+def test_mla_one_decompressed_buffer_is_an_error():
+    d = mla_desc(1, 2, 64, 64, 64, 256)
+    p = 0x100000
+    st = mfa.lib.mfa_mla_forward(ctypes.byref(d), p, p, p, p, p, None, p, None, None)
+    assert st == 4 and b"both" in mfa.lib.mfa_last_error()
+    st = mfa.lib.mfa_mla_forward(ctypes.byref(d), p, p, p, p, None, p, p, None, None)
+    assert st == 4
+
+
+def test_absorbed_workspace_covers_split_partials():
+    # Decode (S_q 1, B 32, H 16): 16 query rows per batch item -> 32 blocks, split keys.
+    dec = mfa.lib.mfa_mla_absorbed_workspace_size(ctypes.byref(mla_desc(32, 16, 1, 4096, 128, 512)))
+    qt = 32 * 16 * 512 * 2
+    assert dec > 2 * qt  # Q~, O~ and the FP32 partials
+    # Prefill (S_q 4096): enough blocks, no split: Q~ and O~ only.
+    pre = mfa.lib.mfa_mla_absorbed_workspace_size(ctypes.byref(mla_desc(1, 16, 4096, 4096, 128, 512)))
+    assert pre == 2 * 16 * 4096 * 512 * 2
