@@ -15,7 +15,7 @@ import torch
 
 import mfa_amd as mfa
 import oracle_lib as ol
-from harness import seen
+from harness import maxerr, seen
 from test_backward_gpu import check_backward, run_backward
 
 pytestmark = pytest.mark.gpu
@@ -151,3 +151,46 @@ def test_c5_full_shard_slice_invariance(gpu):
     sum_do = do.double().sum(dim=2)
     assert (sum_dv - sum_do).abs().max().item() <= 1e-2 * max(1.0, sum_do.abs().max().item())
     assert all(torch.isfinite(t).all() for t in full)
+
+
+@pytest.mark.parametrize("prec", [FP16, BF16])
+def test_config5_full_size_forward_backward(gpu, prec):
+    """BASELINE.json configs[4] per-GPU shard (B8 H32 S4096 D256, non-causal) through the C
+    ABI, forward then backward: one (b, h) slice against the C oracle at full length, and on
+    every slice the size-independent identities of the backward (rows of P sum to one, so
+    sum_k dV_k = sum_r dO_r; rows of dS sum to zero, so sum_k dK_k = 0)."""
+    B, H, S, D = 8, 32, 4096, 256
+    dt = torch.float16 if prec == FP16 else torch.bfloat16
+    g = torch.Generator(device=gpu)
+    g.manual_seed(55)
+    q, k, v, do = ((torch.rand((B, H, S, D), generator=g, device=gpu) * 2 - 1).to(dt)
+                   for _ in range(4))
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=prec)
+    desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+    o = torch.empty((B, H, S, D), dtype=torch.float32, device=gpu)
+    l = torch.empty((B, H, S), dtype=torch.float16, device=gpu)
+    dq, dk, dv = (torch.full_like(o, float("nan")) for _ in range(3))
+    dbuf = torch.empty((B, H, S), dtype=torch.bfloat16, device=gpu)
+    mha = mfa.MultiHeadAttention()
+    mha.forward(desc, q, k, v, o, l)
+    mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf)
+    torch.cuda.synchronize()
+    for t in (o, dq, dk, dv):
+        assert torch.isfinite(t).all()
+    # Identities on every slice (fp32 sums on the GPU).
+    # Bounds relative to the sums of magnitudes: P and dS are rounded to the 16-bit MFMA
+    # operand type, so each identity holds to that type's relative precision.
+    eps = 2e-3 if prec == FP16 else 1.6e-2
+    sdv, sdo = dv.sum(dim=2), do.float().sum(dim=2)
+    assert ((sdv - sdo).abs() <= eps * do.float().abs().sum(dim=2) + 1e-3).all()
+    assert (dk.sum(dim=2).abs() <= eps * dk.abs().sum(dim=2) + 1e-3).all()
+    # One slice against the oracle (the inputs the kernel saw, already rounded).
+    b, h = 3, 17
+    sl = lambda t: t[b:b + 1, h:h + 1].float().cpu().numpy()
+    ref = ol.attention(sl(q), sl(k), sl(v), dO=sl(do))
+    assert maxerr(sl(o), ref["O"]) <= (5e-3 if prec == FP16 else 1e-2)
+    tol = 5e-2 if prec == FP16 else 1e-1
+    for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
+        e = maxerr(sl(t), ref[name])
+        assert e <= tol, f"{name} max error {e} > {tol}"
+    assert maxerr(dbuf[b:b + 1, h:h + 1].float().cpu().numpy(), ref["D"]) <= 1e-1
