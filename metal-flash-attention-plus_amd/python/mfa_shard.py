@@ -67,3 +67,27 @@ def forward_shard(mfa, base, q, k, v, o, l, world: int, rank: int, stream=None) 
                     None if l is None else l[b:b + 1, h0:h1], stream=stream)
         n += h1 - h0
     return n
+
+
+def backward_shard(mfa, base, q, k, v, o, do, l, dq, dk, dv, dbuf, world: int, rank: int,
+                   stream=None) -> int:
+    """Runs this rank's backward slices (backward_slices) through the C ABI: backwardQuery then
+    backwardKeyValue per slice, as mfa_multihead_backward does for the whole batch.  Tensors
+    are the full [B, H, S, D] / [B, H_kv, S_kv, D] device arrays (forward outputs O, L
+    included); each rank writes dQ and D for its query heads and dK / dV for the kv heads it
+    owns.  MHA slices are (b, head range); GQA / MQA slices are whole batch elements, so a kv
+    group's dK / dV sum never crosses ranks and needs no collective.  Returns the number of
+    (b, h) query-head slices processed."""
+    B, H, R, D = q.shape
+    Hkv, C = k.shape[1], k.shape[2]
+    mha = mfa.MultiHeadAttention()
+    n = 0
+    for b, h0, h1 in backward_slices(B, H, Hkv, world, rank):
+        hk0, hk1 = (h0, h1) if Hkv == H else (0, Hkv)
+        desc = mfa.MultiHeadDescriptor.make(base, 1, h1 - h0, R, D, Hkv=hk1 - hk0, C=C)
+        qs = (slice(b, b + 1), slice(h0, h1))
+        ks = (slice(b, b + 1), slice(hk0, hk1))
+        mha.backward(desc, q[qs], k[ks], v[ks], o[qs], do[qs], l[qs], dq[qs], dk[ks], dv[ks],
+                     dbuf[qs], stream=stream)
+        n += h1 - h0
+    return n

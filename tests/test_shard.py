@@ -101,3 +101,51 @@ def test_gloo_world2_sharded_forward_equals_unsharded(B, H, Hkv):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok and tmax == 2.0
+
+
+def _bwd_worker(rank, world, port, B, H, Hkv, S, D, q):
+    """Each rank runs the oracle backward on its backward_slices (standing in for the per-GPU
+    kernels test_shard_gpu.py drives); rank 0 assembles dQ / dK / dV and checks them against
+    the unsharded backward: kv groups never straddle ranks, so no reduction is needed."""
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    rng = np.random.default_rng(11)
+    Q, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(2))
+    K, V = (rng.standard_normal((B, Hkv, S, D)).astype(np.float32) for _ in range(2))
+    pieces = []
+    for b, h0, h1 in sh.backward_slices(B, H, Hkv, world, rank):
+        hk0, hk1 = (h0, h1) if Hkv == H else (0, Hkv)
+        r = ol.attention(Q[b:b + 1, h0:h1], K[b:b + 1, hk0:hk1], V[b:b + 1, hk0:hk1],
+                         causal=True, dO=dO[b:b + 1, h0:h1])
+        pieces.append((b, h0, h1, hk0, hk1, r["dQ"], r["dK"], r["dV"], r["D"]))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, pieces)
+    if rank == 0:
+        dQ = np.full((B, H, S, D), np.nan, dtype=np.float32)
+        dK = np.full((B, Hkv, S, D), np.nan, dtype=np.float32)
+        dV = np.full_like(dK, np.nan)
+        Dt = np.full((B, H, S), np.nan, dtype=np.float32)
+        for plist in gathered:
+            for b, h0, h1, hk0, hk1, gq, gk, gv, gd in plist:
+                dQ[b, h0:h1], Dt[b, h0:h1] = gq[0], gd[0]
+                dK[b, hk0:hk1], dV[b, hk0:hk1] = gk[0], gv[0]
+        full = ol.attention(Q, K, V, causal=True, dO=dO)
+        q.put(all(np.array_equal(x, full[n]) for x, n in
+                  ((dQ, "dQ"), (dK, "dK"), (dV, "dV"), (Dt, "D"))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B,H,Hkv", [(2, 4, 4), (3, 4, 2), (2, 4, 1)])
+def test_gloo_world2_sharded_backward_equals_unsharded(B, H, Hkv):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bwd_worker, args=(r, 2, port, B, H, Hkv, 40, 16, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok
