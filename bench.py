@@ -148,8 +148,8 @@ def main():
             "workload": "INT8 K/V (per-tensor, zp 0) + fp16 Q, H16 S8192 D128 non-causal "
                         "(BASELINE configs[2])",
             "int8_kernel": mfa.quantized_plan(qdesc, mfa.KernelType.forward, tq, tk, tv)[0]["name"],
-            "int8_dequant_exact_kernel": mfa.quantized_plan(qdesc_exact, mfa.KernelType.forward,
-                                                            tq, tk, tv)[0]["name"],
+            "int8_dequant_exact_kernels": [r["name"] for r in mfa.quantized_plan(
+                qdesc_exact, mfa.KernelType.forward, tq, tk, tv)],
             "int8_tops": round(f3 / (ms_i8 * 1e-3) / 1e12, 2),
             "int8_roofline_frac": round(f3 / (ms_i8 * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4),
             "fp16_tflops_same_shape": round(f3 / (ms_f16 * 1e-3) / 1e12, 2),
@@ -194,6 +194,58 @@ def main():
             "ms_per_step": round(el5 / n5 * 1e3, 3),
         }
         del q5, k5, v5, do5, o5, l5, dq5, dk5, dv5, db5
+
+    # --------------------------------------------- quantized fwd + bwd (INT8 K/V) vs fp16
+    if not args.no_c5 and not args.no_int8:
+        Bq, Hq, Sq, Dq = 2, 32, 4096, 256
+        q8, do8 = (uniform((Bq, Hq, Sq, Dq), torch.float16) for _ in range(2))
+        kf8 = uniform((Bq, Hq, Sq, Dq), torch.float32)
+        vf8 = uniform((Bq, Hq, Sq, Dq), torch.float32)
+        k8, ks8, _, _ = mfa.quantize(kf8, mfa.Precision.INT8, rows=Bq * Hq * Sq, cols=Dq)
+        v8, vs8, _, _ = mfa.quantize(vf8, mfa.Precision.INT8, rows=Bq * Hq * Sq, cols=Dq)
+        kh8, vh8 = kf8.half(), vf8.half()
+        del kf8, vf8
+        o8 = torch.empty((Bq, Hq, Sq, Dq), dtype=torch.float32, device=dev)
+        l8 = torch.empty((Bq, Hq, Sq), dtype=torch.float16, device=dev)
+        dq8, dk8, dv8 = (torch.empty_like(o8) for _ in range(3))
+        db8 = torch.empty((Bq, Hq, Sq), dtype=torch.bfloat16, device=dev)
+        base8 = mfa.AttentionDescriptor.make(Sq, Sq, Dq, low_precision=True,
+                                             precision=mfa.Precision.FP16)
+        qd8 = mfa.quantized_descriptor(base8, mfa.Precision.FP16, mfa.Precision.INT8,
+                                       mfa.Precision.INT8, B=Bq, H=Hq)
+        tq8 = mfa.quantized_tensor(q8, mfa.Precision.FP16)
+        tk8 = mfa.quantized_tensor(k8, mfa.Precision.INT8, scale=float(ks8.item()))
+        tv8 = mfa.quantized_tensor(v8, mfa.Precision.INT8, scale=float(vs8.item()))
+        qa8 = mfa.QuantizedAttention()
+        desc8 = mfa.MultiHeadDescriptor.make(base8, Bq, Hq, Sq, Dq)
+
+        def step_q8():
+            qa8.forward(qd8, tq8, tk8, tv8, o8, l8, stream=stream)
+            qa8.backwardQuery(qd8, tq8, tk8, tv8, o8, do8, l8, dq8, db8, stream=stream)
+            qa8.backwardKeyValue(qd8, tq8, tk8, tv8, do8, l8, db8, dk8, dv8, stream=stream)
+
+        def step_f16():
+            mha.forward(desc8, q8, kh8, vh8, o8, l8, stream=stream)
+            mha.backward(desc8, q8, kh8, vh8, o8, do8, l8, dq8, dk8, dv8, db8, stream=stream)
+
+        ms_q8 = ev_time(step_q8)
+        plan_q8 = [r["name"] for kind in (mfa.KernelType.forward, mfa.KernelType.backwardQuery,
+                                          mfa.KernelType.backwardKeyValue)
+                   for r in mfa.quantized_plan(qd8, kind, tq8, tk8, tv8)]
+        ms_f8 = ev_time(step_f16)
+        f8 = (mfa.attention_flops(Bq, Hq, Sq, Sq, Dq) +
+              mfa.attention_flops(Bq, Hq, Sq, Sq, Dq, kind="backward"))
+        result["int8_fwd_bwd_d256"] = {
+            "workload": f"QuantizedAttention forward + backwardQuery + backwardKeyValue, INT8 "
+                        f"K/V (per-tensor) + fp16 Q/dO, B{Bq} H{Hq} S{Sq} D{Dq} non-causal "
+                        f"(C5-like), against MultiHeadAttention fp16 forward + backward",
+            "int8_tflops": round(f8 / (ms_q8 * 1e-3) / 1e12, 2),
+            "fp16_tflops": round(f8 / (ms_f8 * 1e-3) / 1e12, 2),
+            "ratio_int8_over_fp16": round(ms_f8 / ms_q8, 3),
+            "int8_ms": round(ms_q8, 3), "fp16_ms": round(ms_f8, 3),
+            "int8_kernels": plan_q8,
+        }
+        del q8, do8, k8, v8, kh8, vh8, o8, l8, dq8, dk8, dv8, db8
 
     # ---------------------------------------------------------------- C4: MLA
     if not args.no_mla:

@@ -645,6 +645,37 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
          ((uintptr_t)p.v.ptr % 4 == 0);
 }
 
+// Quantised operands go through one dequantisation pass into a dense 16-bit copy
+// (kv_dequant.hip) when the compute type is 16-bit, D % 8 == 0 and each kv head serves at
+// least 128 query rows: every element is then converted once per call instead of once per
+// query block that reads it, and the tuned 16-bit kernels run (bit-identical operands).
+// Decode-like shapes (few query rows) keep reading the quantised tensors directly.
+bool dequant_pass_worth(int R, int H, int Hkv, int D, int elem) {
+  if (const char* e = getenv("MFA_NO_DEQUANT_PASS")) {
+    if (e[0] == '1') return false;
+  }
+  return (elem == 1 || elem == 2) && D % 8 == 0 && D <= 256 && (int64_t)R * (H / Hkv) >= 128;
+}
+
+// Replaces a quantised *op ([B, Hx, S, D]) by a dense 16-bit operand over this stream's
+// scratch `slot`, filled by one kv_dequant launch.  Folded per-tensor scales stay folded.
+mfa_status_t dequant_copy(mfa::Operand* op, int B, int Hx, int S, int D, int elem, int slot,
+                          hipStream_t stream) {
+  void* buf = nullptr;
+  if (mfa::plan_capture()) {
+    buf = (void*)kPlanDummy;
+  } else {
+    const mfa_status_t st = scratch((size_t)B * Hx * S * D * 2, &buf, slot, stream);
+    if (st != MFA_SUCCESS) return st;
+  }
+  const mfa_status_t st =
+      hip_status(mfa::kv_dequant_dispatch(*op, B, Hx, S, D, elem, buf, stream), "dequant pass");
+  if (st != MFA_SUCCESS) return st;
+  *op = make_operand(buf, elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16, B, Hx, S, D,
+                     nullptr, 0);
+  return MFA_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* desc,
@@ -713,7 +744,18 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     return hip_status(mfa::fwd_i8mma_dispatch(pi, elem, (hipStream_t)stream),
                       "mfa_fwd (integer matmul) launch");
   }
-  return hip_status(launch_forward(p, elem, DP, src_kind(kp), (hipStream_t)stream),
+  int kvsrc = src_kind(kp);
+  if (dequant_pass_worth(R, H, Hkv, D, elem)) {
+    hipStream_t s = (hipStream_t)stream;
+    if (kvsrc > 0) {
+      if ((st = dequant_copy(&p.k, B, Hkv, C, D, elem, 6, s)) != MFA_SUCCESS) return st;
+      if ((st = dequant_copy(&p.v, B, Hkv, C, D, elem, 7, s)) != MFA_SUCCESS) return st;
+      kvsrc = 0;
+    }
+    if (is_quantized(qp) && (st = dequant_copy(&p.q, B, H, R, D, elem, 8, s)) != MFA_SUCCESS)
+      return st;
+  }
+  return hip_status(launch_forward(p, elem, DP, kvsrc, (hipStream_t)stream),
                     "mfa_fwd (quantized) launch");
 }
 
@@ -965,7 +1007,20 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   p.dq_mul = fk;
   p.dk_mul = fq;
   if ((st = plan_masks(base, nullptr, R, C, &p.mask)) != MFA_SUCCESS) return st;
-  return run_backward(p, elem, DP, src_kind(kp), src_kind(qp), phase, (hipStream_t)stream);
+  int ksrc = src_kind(kp), qsrc = src_kind(qp);
+  if (dequant_pass_worth(R, H, Hkv, D, elem)) {
+    hipStream_t s = (hipStream_t)stream;
+    if (ksrc > 0) {
+      if ((st = dequant_copy(&p.k, B, Hkv, C, D, elem, 6, s)) != MFA_SUCCESS) return st;
+      if ((st = dequant_copy(&p.v, B, Hkv, C, D, elem, 7, s)) != MFA_SUCCESS) return st;
+      ksrc = 0;
+    }
+    if (qsrc > 0) {
+      if ((st = dequant_copy(&p.q, B, H, R, D, elem, 8, s)) != MFA_SUCCESS) return st;
+      qsrc = 0;
+    }
+  }
+  return run_backward(p, elem, DP, ksrc, qsrc, phase, (hipStream_t)stream);
 }
 
 }  // namespace

@@ -55,6 +55,10 @@ int bwd_lds_bytes(int kind, int elem, int DP);
 hipError_t bwd_fast_dispatch(const BwdParams& p, int kind, int elem, int DP, hipStream_t stream);
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
+// Dense 16-bit copy [B, Hx, S, D] of a quantised operand holding the MFMA operands the
+// dequantise-on-load staging would produce (kv_dequant.hip).
+hipError_t kv_dequant_dispatch(const Operand& op, int B, int Hx, int S, int D, int elem,
+                               void* out, hipStream_t stream);
 // Third-generation 16-bit forward at D = 128, no mask or causal (attention_fwd_v3.hip);
 // hipErrorNotSupported otherwise.
 hipError_t fwd3_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);

@@ -103,10 +103,10 @@ inline void kernel_symbol_name(const void* handle, char* out, size_t n) {
   snprintf(out, n, "%s", s.c_str());
 }
 
-// Launches kern<<<grid, block, lds, stream>>>(params), or records it while a plan is captured.
-template <class K, class P>
+// Launches kern<<<grid, block, lds, stream>>>(args...), or records it while a plan is captured.
+template <class K, class... Args>
 inline hipError_t launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
-                         const P& params) {
+                         const Args&... args) {
   if (PlanCapture* cap = plan_capture()) {
     if (cap->count < PlanCapture::kMax) {
       LaunchRec& r = cap->rec[cap->count++];
@@ -121,7 +121,7 @@ inline hipError_t launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t 
     hipError_t e = set_lds_attr_per_device(kern, lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, block, lds, stream, params);
+  hipLaunchKernelGGL(kern, grid, block, lds, stream, args...);
   LaunchLog& log = launch_log();
   const int i = (int)(log.total++ % LaunchLog::kMax);
   log.handle[i] = (const void*)kern;

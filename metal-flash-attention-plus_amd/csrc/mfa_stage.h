@@ -91,6 +91,71 @@ __device__ __forceinline__ uint4 dequant_fast(const uint4 raw, float zp) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// One 8-element chunk (columns d0..d0+7 of the row at element offset rowoff) of a quantised
+// operand: INT8 bytes in .x/.y, or eight INT4 nibbles in .x (columns past D decode to 0).
+template <int SRC>
+__device__ __forceinline__ uint4 load_qchunk(const Operand& op, int64_t rowoff, int d0, int D) {
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (SRC == SRC_I8) {
+    const int8_t* base = (const int8_t*)op.ptr + rowoff;
+    if (op.vec && d0 + 8 <= D) {
+      const uint2 t = *reinterpret_cast<const uint2*>(base + d0);
+      v.x = t.x; v.y = t.y;
+    } else {
+      uint32_t w[2] = {0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (d0 + j < D) w[j >> 2] |= (uint32_t)(uint8_t)base[(int64_t)(d0 + j) * op.sd] << (8 * (j & 3));
+      v.x = w[0]; v.y = w[1];
+    }
+  } else {  // SRC_I4: element index e -> byte e/2, low nibble = even element
+    const uint8_t* base = (const uint8_t*)op.ptr;
+    uint32_t w = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (d0 + j < D) {
+        const int64_t e = rowoff + (int64_t)(d0 + j) * op.sd;
+        const uint8_t byte = base[e >> 1];
+        const uint32_t nib = (e & 1) ? (byte >> 4) : (byte & 15);
+        w |= nib << (4 * j);
+      } else {
+        w |= 8u << (4 * j);  // decodes to 0
+      }
+    v.x = w;
+  }
+  return v;
+}
+
+// The MFMA-type chunk of a quantised chunk: per-tensor the exact integers q - zp (the scale is
+// folded by the host); blockwise the dequantised value (q - zp)·s rounded to the element type.
+// `row2d` is the row of the [rows, cols] quantisation view; invalid rows give zeros.
+template <class E, int SRC>
+__device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& op, int64_t row2d,
+                                                int d0, int D, bool valid) {
+  if (!op.bscale) return dequant_fast<E, SRC>(raw, (float)op.zp);
+  uint32_t w[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    uint32_t packed = 0u;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = 2 * jj + e;
+      int qv;
+      if constexpr (SRC == SRC_I8) {
+        const uint32_t word = j < 4 ? raw.x : raw.y;
+        qv = (int)(int8_t)((word >> (8 * (j & 3))) & 0xff);
+      } else {
+        qv = (int)((raw.x >> (4 * j)) & 15u) - 8;
+      }
+      float x = 0.f;
+      if (valid && d0 + j < D) x = dequant(op, qv, row2d, d0 + j);
+      packed |= (uint32_t)E::from_f32(x) << (16 * e);
+    }
+    w[jj] = packed;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 template <class A, int ROWS, int DP, int NT, int SRC>
 struct Stager {
   static constexpr int CE = 16 / A::ESIZE;   // output elements per 16-byte chunk
@@ -157,32 +222,8 @@ struct Stager {
             }
             v = make_uint4(w[0], w[1], w[2], w[3]);
           }
-        } else if constexpr (SRC == SRC_I8) {
-          const int8_t* base = (const int8_t*)op.ptr + rowoff;
-          if (op.vec && d0 + 8 <= D) {
-            const uint2 t = *reinterpret_cast<const uint2*>(base + d0);
-            v.x = t.x; v.y = t.y;
-          } else {
-            uint32_t w[2] = {0u, 0u};
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (d0 + j < D) w[j >> 2] |= (uint32_t)(uint8_t)base[(int64_t)(d0 + j) * op.sd] << (8 * (j & 3));
-            v.x = w[0]; v.y = w[1];
-          }
-        } else {  // SRC_I4: element index e -> byte e/2, low nibble = even element
-          const uint8_t* base = (const uint8_t*)op.ptr;
-          uint32_t w = 0u;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (d0 + j < D) {
-              const int64_t e = rowoff + (int64_t)(d0 + j) * op.sd;
-              const uint8_t byte = base[e >> 1];
-              const uint32_t nib = (e & 1) ? (byte >> 4) : (byte & 15);
-              w |= nib << (4 * j);
-            } else {
-              w |= 8u << (4 * j);  // decodes to 0
-            }
-          v.x = w;
+        } else {
+          v = load_qchunk<SRC>(op, rowoff, d0, D);
         }
       }
       raw[i] = v;
@@ -223,37 +264,15 @@ struct Stager {
           } else {
             out = raw[i];
           }
-        } else if (!op.bscale) {
-          // Per-tensor: the staged value is the exact integer (q - zp); zero-filled loads
-          // beyond the tile edge only ever meet zero Q columns or masked keys.
-          out = dequant_fast<typename A::Elem, SRC>(raw[i], (float)op.zp);
         } else {
+          // Per-tensor: the exact integers (q - zp); zero-filled loads beyond the tile edge
+          // only ever meet zero Q columns or masked keys.
           const int grow = row0 + r;
-          const int d0 = c * 8;
-          const bool valid = grow < nrows;
           const int64_t row2d =
-              ((int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss) / op.cols;
-          uint32_t w[4];
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            uint32_t packed = 0u;
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int j = 2 * jj + e;
-              int qv;
-              if constexpr (SRC == SRC_I8) {
-                const uint32_t word = j < 4 ? raw[i].x : raw[i].y;
-                qv = (int)(int8_t)((word >> (8 * (j & 3))) & 0xff);
-              } else {
-                qv = (int)((raw[i].x >> (4 * j)) & 15u) - 8;
-              }
-              float x = 0.f;
-              if (valid && d0 + j < D) x = dequant(op, qv, row2d, d0 + j);
-              packed |= (uint32_t)A::Elem::from_f32(x) << (16 * e);
-            }
-            w[jj] = packed;
-          }
-          out = make_uint4(w[0], w[1], w[2], w[3]);
+              op.bscale
+                  ? ((int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss) / op.cols
+                  : 0;
+          out = convert_qchunk<typename A::Elem, SRC>(raw[i], op, row2d, c * 8, D, grow < nrows);
         }
         *reinterpret_cast<uint4*>(tile + A::TileT::off(r, c)) = out;
       }

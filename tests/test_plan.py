@@ -79,14 +79,27 @@ def test_quantized_plans():
     base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
     qi = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, integer_matmul=True)
     assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 64, 3>"
+    # Dequant-exact: one dequantisation pass per quantised operand (kv_dequant.hip), then the
+    # tuned 16-bit kernel on the dense copies.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
-    assert one(mfa.quantized_plan(qx))["name"] == "mfa_fwd_fast_kernel<F16, 128, 64, 1>"
-    # Backward of quantized K/V runs the generic kernels with the INT8 source.
-    assert one(mfa.quantized_plan(qx, K.backwardQuery))["name"].startswith("mfa_bwd_q_kernel<")
-    # A non-zero zero point leaves the integer-matmul kernel.
+    names = [r["name"] for r in mfa.quantized_plan(qx)]
+    assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
+    assert names[2].startswith("mfa_fwd2_kernel<F16, 128, 64, 2") and len(names) == 3
+    for kind, kern in ((K.backwardQuery, "mfa_bwd_q_fast_kernel<F16, 128, 64>"),
+                       (K.backwardKeyValue, "mfa_bwd_kv_fast_kernel<F16, 128, 64>")):
+        assert [r["name"] for r in mfa.quantized_plan(qx, kind)][2] == kern
+    # INT4 and a quantised Q take the same pass (SRC_I4 = 2).
+    q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
+    names = [r["name"] for r in mfa.quantized_plan(q4)]
+    assert names[:3] == ["mfa_kv_dequant_kernel<F16, 2>"] * 2 + ["mfa_kv_dequant_kernel<F16, 1>"]
+    assert names[3].startswith("mfa_fwd2_kernel<F16, 128")
+    # A non-zero zero point leaves the integer-matmul kernel (dequant-exact path instead).
     zp = mfa.QuantizedTensor(None, int(P.INT8), 0.5, 3)
-    assert one(mfa.quantized_plan(qi, K.forward, None, zp, zp))["name"].startswith(
-        "mfa_fwd_fast_kernel<")
+    assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_kernel<")
+    # Decode-like shapes (few query rows per kv head) read the quantised tensors directly.
+    dec = mfa.AttentionDescriptor.make(16, 8192, 128, low_precision=True, precision=P.FP16)
+    qd = mfa.quantized_descriptor(dec, P.FP16, P.INT8, P.INT8, B=1, H=4)
+    assert one(mfa.quantized_plan(qd))["name"].startswith("mfa_fwd_fast_kernel<")
 
 
 def test_environment_override_is_visible_in_plan(monkeypatch):

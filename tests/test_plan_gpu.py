@@ -83,9 +83,12 @@ def test_int8_launches_match_plan(gpu, integer_matmul):
     mfa.last_launches()
     mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
     torch.cuda.synchronize()
-    assert mfa.last_launches() == plan and len(plan) == 1
-    want = "mfa_fwd_i8_kernel<" if integer_matmul else "mfa_fwd_fast_kernel<"
-    assert plan[0]["name"].startswith(want)
+    assert mfa.last_launches() == plan
+    if integer_matmul:
+        assert len(plan) == 1 and plan[0]["name"].startswith("mfa_fwd_i8_kernel<")
+    else:  # dequantisation pass for K and V, then the tuned 16-bit forward
+        assert [r["name"] for r in plan[:2]] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
+        assert len(plan) == 3 and plan[2]["name"].startswith("mfa_fwd2_kernel<F16, 128")
 
 
 @pytest.mark.parametrize("D,causal", [(128, True), (256, False)])

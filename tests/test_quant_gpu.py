@@ -301,6 +301,72 @@ def test_quantized_backward_dequant_exact(gpu):
         assert maxerr(t, ref[name]) < 5e-2, name
 
 
+# ----------------------------------------------------------------------- dequantisation pass
+# Shapes with >= 128 query rows per kv head dequantise K/V (and a quantised Q) once into dense
+# 16-bit copies (kv_dequant.hip) and run the tuned 16-bit kernels; the copies hold exactly the
+# operands dequantise-on-load staging produces, so the result matches the direct path up to
+# the two kernels' summation orders.
+def test_dequant_pass_matches_direct_path(gpu, monkeypatch):
+    B, H, S, D = 1, 4, 256, 128
+    rng = np.random.default_rng(21)
+    Q, K, V = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
+    for kv in (P.INT8, P.INT4):
+        o1, l1, deq, _ = run_qforward(Q, K, V, P.FP16, kv, kv, causal=True)
+        monkeypatch.setenv("MFA_NO_DEQUANT_PASS", "1")
+        o2, l2, _, _ = run_qforward(Q, K, V, P.FP16, kv, kv, causal=True)
+        monkeypatch.delenv("MFA_NO_DEQUANT_PASS")
+        assert maxerr(o1, o2.cpu().numpy()) < 2e-3
+        ref = ol.attention(deq["Q"], deq["K"], deq["V"], causal=True)
+        assert maxerr(o1, ref["O"]) < 2e-2 and maxerr(l1, ref["L"]) < 1e-2
+
+
+def test_dequant_pass_blockwise_and_quantized_query(gpu):
+    B, H, S, D, bs = 1, 2, 256, 64, 16
+    rng = np.random.default_rng(22)
+    Q, K, V = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
+    o, l, deq, _ = run_qforward(Q, K, V, P.INT8, P.INT8, P.INT8, blockwise=bs)
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"])
+    assert maxerr(o, ref["O"]) < 2e-2 and maxerr(l, ref["L"]) < 1e-2
+
+
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+def test_dequant_pass_backward_on_fast_kernels(gpu, kv):
+    """Low-precision descriptor (FP16 Q and dO): after the pass the backward runs the tuned
+    kernels (plan checked) and matches the oracle on the dequantised values."""
+    B, H, S, D = 1, 2, 256, 128
+    rng = np.random.default_rng(23)
+    Q, K, V, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) * 0.5 for _ in range(4))
+    kq, ks, kd = quantize_host(K, kv)
+    vq, vs, vd = quantize_host(V, kv)
+    Qd, dOd = seen(Q, P.FP16), seen(dO, P.FP16)
+    ref = ol.attention(Qd, kd, vd, dO=dOd, causal=True)
+    base = mfa.AttentionDescriptor.make(S, S, D, causal=True, low_precision=True,
+                                        precision=P.FP16)
+    desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H)
+    kt, vt = tdev(kq, torch.uint8), tdev(vq, torch.uint8)
+    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    tk = mfa.quantized_tensor(kt, kv, scale=ks)
+    tv = mfa.quantized_tensor(vt, kv, scale=vs)
+    o = tdev(ref["O"])
+    l = torch.from_numpy(ref["L"]).half().to(DEV)
+    do = to_device(dO, P.FP16)
+    dq = torch.empty((B, H, S, D), dtype=torch.float32, device=DEV)
+    dk, dv = torch.empty_like(dq), torch.empty_like(dq)
+    dvals = torch.empty((B, H, S), dtype=torch.bfloat16, device=DEV)
+    qa = mfa.QuantizedAttention()
+    plan = (mfa.quantized_plan(desc, mfa.KernelType.backwardQuery, tq, tk, tv) +
+            mfa.quantized_plan(desc, mfa.KernelType.backwardKeyValue, tq, tk, tv))
+    assert plan[2]["name"].startswith("mfa_bwd_q_fast_kernel<F16, 128")
+    assert plan[5]["name"].startswith("mfa_bwd_kv_fast_kernel<F16, 128")
+    mfa.last_launches()
+    qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
+    qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
+    torch.cuda.synchronize()
+    assert mfa.last_launches() == plan[2:]  # the log keeps the last four launches
+    for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
+        assert maxerr(t, ref[name]) < 5e-2, name
+
+
 # ----------------------------------------------------------------------- integer matmul
 # The INT8-MFMA forward (attention_fwd_i8.hip) quantises Q per row and P to INT8 (P' =
 # round(127 P) against a max rounded up to an integer, so 6-7 bits), so it is not
