@@ -40,7 +40,7 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 template <class E, int DP, int BK, int OCC>
 __global__ void __launch_bounds__(256, OCC) mfa_fwd_i8_kernel(FwdParams p) {
-  static_assert(DP == 128 && BK == 64, "int8 kernel is specialised for D<=128, 64-key tiles");
+  static_assert(DP == 128 && (BK == 64 || BK == 128), "int8 kernel: D<=128, 64/128-key tiles");
   using TK = Tile16<DP / 2>;            // [BK][DP bytes] = 16-byte chunks, DP/16 per row
   constexpr int NT = 256, BQ = 128;
   constexpr int NJ = BK / 32;
@@ -309,19 +309,22 @@ __global__ void __launch_bounds__(256, OCC) mfa_fwd_i8_kernel(FwdParams p) {
   }
 }
 
-template <class E, int OCC>
+template <class E, int BK, int OCC>
 static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
-  constexpr int LDS = 2 * (64 * 128) + 2 * (128 * 64);
-  auto kern = mfa_fwd_i8_kernel<E, 128, 64, OCC>;
+  constexpr int LDS = 4 * BK * 128;  // K and V, double-buffered
+  auto kern = mfa_fwd_i8_kernel<E, 128, BK, OCC>;
   return launch(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
 }
 
 // INT8-MFMA forward: Q fp16/bf16 (quantised per row in-kernel), K/V INT8 per-tensor with zero
-// point 0, D <= 128, D % 16 == 0.
+// point 0, D <= 128, D % 16 == 0.  128-key tiles at 2 waves per SIMD (228 VGPRs, 64 KiB LDS)
+// measured +2 % over 64-key tiles at 3 waves per SIMD (165 VGPRs) at C3 (1616-1622 vs
+// 1584-1589 TOPS, two one-process A/B runs); MFA_I8_BK=64 selects the latter.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) {
-  // 3 waves per SIMD: the kernel fits in 168 VGPRs and 3 x 32 KiB of LDS per CU.
-  if (elem == P_FP16) return launch_i8<F16, 3>(p, stream);
-  if (elem == P_BF16) return launch_i8<BF16, 3>(p, stream);
+  const char* bk = getenv("MFA_I8_BK");
+  const bool small = bk && bk[0] == '6';
+  if (elem == P_FP16) return small ? launch_i8<F16, 64, 3>(p, stream) : launch_i8<F16, 128, 2>(p, stream);
+  if (elem == P_BF16) return small ? launch_i8<BF16, 64, 3>(p, stream) : launch_i8<BF16, 128, 2>(p, stream);
   return hipErrorNotSupported;
 }
 
@@ -329,5 +332,7 @@ hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) 
 // that are only named through a launch helper).
 template __global__ void mfa_fwd_i8_kernel<F16, 128, 64, 3>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<BF16, 128, 64, 3>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<F16, 128, 128, 2>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<BF16, 128, 128, 2>(FwdParams);
 
 }  // namespace mfa

@@ -78,7 +78,7 @@ def test_misaligned_query_falls_back_to_generic_kernel():
 def test_quantized_plans():
     base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
     qi = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, integer_matmul=True)
-    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 64, 3>"
+    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 128, 2>"
     # Dequant-exact: one dequantisation pass per quantised operand (kv_dequant.hip), then the
     # tuned 16-bit kernel on the dense copies.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
