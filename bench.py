@@ -126,6 +126,8 @@ def main():
         l3 = torch.empty((B, H, S3), dtype=torch.float16, device=dev)
         kq, ks, _, _ = mfa.quantize(kf, mfa.Precision.INT8, rows=B * H * S3, cols=D)
         vq, vs, _, _ = mfa.quantize(vf, mfa.Precision.INT8, rows=B * H * S3, cols=D)
+        k4, ks4, _, _ = mfa.quantize(kf, mfa.Precision.INT4, rows=B * H * S3, cols=D)
+        v4, vs4, _, _ = mfa.quantize(vf, mfa.Precision.INT4, rows=B * H * S3, cols=D)
         torch.cuda.synchronize()
         base3 = mfa.AttentionDescriptor.make(S3, S3, D, low_precision=True,
                                              precision=mfa.Precision.FP16)
@@ -139,9 +141,14 @@ def main():
         tv = mfa.quantized_tensor(vq, mfa.Precision.INT8, scale=float(vs.item()))
         kh, vh = kf.half(), vf.half()
         desc3 = mfa.MultiHeadDescriptor.make(base3, B, H, S3, D)
+        qdesc4 = mfa.quantized_descriptor(base3, mfa.Precision.FP16, mfa.Precision.INT4,
+                                          mfa.Precision.INT4, B=B, H=H)
+        tk4 = mfa.quantized_tensor(k4, mfa.Precision.INT4, scale=float(ks4.item()))
+        tv4 = mfa.quantized_tensor(v4, mfa.Precision.INT4, scale=float(vs4.item()))
 
         ms_i8 = ev_time(lambda: qa.forward(qdesc, tq, tk, tv, o3, l3, stream=stream))
         ms_i8x = ev_time(lambda: qa.forward(qdesc_exact, tq, tk, tv, o3, l3, stream=stream))
+        ms_i4 = ev_time(lambda: qa.forward(qdesc4, tq, tk4, tv4, o3, l3, stream=stream))
         ms_f16 = ev_time(lambda: mha.forward(desc3, qf, kh, vh, o3, l3, stream=stream))
         f3 = mfa.attention_flops(B, H, S3, S3, D, causal=False)
         result["int8"] = {
@@ -155,10 +162,12 @@ def main():
             "fp16_tflops_same_shape": round(f3 / (ms_f16 * 1e-3) / 1e12, 2),
             "ratio_int8_over_fp16": round(ms_f16 / ms_i8, 3),
             "int8_dequant_exact_tflops": round(f3 / (ms_i8x * 1e-3) / 1e12, 2),
+            "int4_dequant_exact_tflops": round(f3 / (ms_i4 * 1e-3) / 1e12, 2),
             "int8_ms": round(ms_i8, 4), "int8_dequant_exact_ms": round(ms_i8x, 4),
+            "int4_dequant_exact_ms": round(ms_i4, 4),
             "fp16_ms": round(ms_f16, 4),
         }
-        del qf, kf, vf, o3, l3, kq, vq, kh, vh
+        del qf, kf, vf, o3, l3, kq, vq, kh, vh, k4, v4
 
     # ---------------------------------------------------------------- C5: fwd + bwd, D=256
     if not args.no_c5:
