@@ -94,41 +94,46 @@ struct NoHook {
   __device__ __forceinline__ void operator()(int) const {}
 };
 
+// One tile in three parts: fwd2_qk (S^T = K·Q^T; S·c − moff on the fp16 path), fwd2_softmax
+// (masks, online softmax, P packed as the PV B operand) and fwd2_pv (O^T += V^T·P^T).
 // qk_hook(i) runs after QK^T MFMA i (e.g. staging the next tile piece by piece).
 template <class E, int DP, int BK, class TU = TuneDefault, class QKHook = NoHook>
-__device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const int (&rbase)[2],
-                                          const int (&trb)[2], const i16x8 (&qf)[DP / 16],
-                                          RowState<DP>& st, int t, bool mask_tile, int qi,
-                                          const FwdParams& p, float c, int wsz, int hh,
-                                          QKHook&& qk_hook = QKHook()) {
+__device__ __forceinline__ void fwd2_qk(const char* kt, const int (&rbase)[2],
+                                        const i16x8 (&qf)[DP / 16], const RowState<DP>& st,
+                                        f32x16 (&s)[BK / 32], QKHook&& qk_hook = QKHook()) {
   using A = Arith16<E, DP>;
   // Pre-scaled Q, S' = S·c − moff from the MFMA (fp16 up to D=128: at D=256 the −m tile's
   // registers are worth more than the per-element multiply-add, which halves per MFMA there).
   constexpr bool PS = E::prec == P_FP16 && DP <= 128;
-  constexpr int NJ = BK / 32, DS = DP / 16, ND = DP / 32;
-  constexpr float THR = 8.0f;
-  f32x16 s[NJ];
-  {
-    constexpr int NM = DS * NJ;
-    constexpr int AH = DP > 128 ? 2 : TU::AHK;
-    i16x8 kf[AH];
+  constexpr int NJ = BK / 32, DS = DP / 16;
+  constexpr int NM = DS * NJ;
+  constexpr int AH = DP > 128 ? 2 : TU::AHK;
+  i16x8 kf[AH];
 #pragma unroll
-    for (int i = 0; i < AH; ++i) kf[i] = A::read_row_a(kt, rbase, i % NJ, i / NJ);
-    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
+  for (int i = 0; i < AH; ++i) kf[i] = A::read_row_a(kt, rbase, i % NJ, i / NJ);
+  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < NM; ++i) {
-      const int ds = i / NJ, j = i % NJ;
-      if (ds == 0)
-        s[j] = A::mma(kf[i % AH], qf[0], PS ? st.negm : zero16());
-      else
-        s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
-      if (i + AH < NM) kf[i % AH] = A::read_row_a(kt, rbase, (i + AH) % NJ, (i + AH) / NJ);
-      qk_hook(i);
-      if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
+  for (int i = 0; i < NM; ++i) {
+    const int ds = i / NJ, j = i % NJ;
+    if (ds == 0)
+      s[j] = A::mma(kf[i % AH], qf[0], PS ? st.negm : zero16());
+    else
+      s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
+    if (i + AH < NM) kf[i % AH] = A::read_row_a(kt, rbase, (i + AH) % NJ, (i + AH) / NJ);
+    qk_hook(i);
+    if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
+}
 
+template <class E, int DP, int BK>
+__device__ __forceinline__ void fwd2_softmax(RowState<DP>& st, f32x16 (&s)[BK / 32],
+                                             i16x8 (&pb)[BK / 16], int t, bool mask_tile, int qi,
+                                             const FwdParams& p, float c, int wsz, int hh) {
+  using A = Arith16<E, DP>;
+  constexpr bool PS = E::prec == P_FP16 && DP <= 128;
+  constexpr int NJ = BK / 32, ND = DP / 32;
+  constexpr float THR = 8.0f;
   if (mask_tile) {
     MFA_KEEP_BRANCH();
     // Keys t + 4hh + kk stay for lo <= kk <= hi: below C, at most qi (causal), at least
@@ -182,34 +187,50 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
       rs[i & 3] += pv;
     }
   st.lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) pb[j * 2 + ks] = A::pack(s[j], ks);
+}
 
-  {
-    constexpr int NM = NJ * 2 * ND;
-    constexpr int AH = DP > 128 ? 2 : TU::AHV;
-    i16x8 pb[NJ * 2];
+template <class E, int DP, int BK, class TU = TuneDefault>
+__device__ __forceinline__ void fwd2_pv(const char* vt, const int (&trb)[2],
+                                        const i16x8 (&pb)[BK / 16], RowState<DP>& st) {
+  using A = Arith16<E, DP>;
+  constexpr int NJ = BK / 32, ND = DP / 32;
+  constexpr int NM = NJ * 2 * ND;
+  constexpr int AH = DP > 128 ? 2 : TU::AHV;
+  i16x8 vf[AH];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) pb[j * 2 + ks] = A::pack(s[j], ks);
-    i16x8 vf[AH];
-#pragma unroll
-    for (int i = 0; i < AH; ++i) {
-      const int jk = i / ND, dt = i % ND;
-      vf[i] = A::read_tr_a(vt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
-    }
-    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-      const int jk = i / ND, dt = i % ND;
-      st.o[dt] = A::mma(vf[i % AH], pb[jk], st.o[dt]);
-      if (i + AH < NM) {
-        const int jn = (i + AH) / ND, dn = (i + AH) % ND;
-        vf[i % AH] = A::read_tr_a(vt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
-      }
-      if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
+  for (int i = 0; i < AH; ++i) {
+    const int jk = i / ND, dt = i % ND;
+    vf[i] = A::read_tr_a(vt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
   }
+  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const int jk = i / ND, dt = i % ND;
+    st.o[dt] = A::mma(vf[i % AH], pb[jk], st.o[dt]);
+    if (i + AH < NM) {
+      const int jn = (i + AH) / ND, dn = (i + AH) % ND;
+      vf[i % AH] = A::read_tr_a(vt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
+    }
+    if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
+template <class E, int DP, int BK, class TU = TuneDefault, class QKHook = NoHook>
+__device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const int (&rbase)[2],
+                                          const int (&trb)[2], const i16x8 (&qf)[DP / 16],
+                                          RowState<DP>& st, int t, bool mask_tile, int qi,
+                                          const FwdParams& p, float c, int wsz, int hh,
+                                          QKHook&& qk_hook = QKHook()) {
+  f32x16 s[BK / 32];
+  i16x8 pb[BK / 16];
+  fwd2_qk<E, DP, BK, TU>(kt, rbase, qf, st, s, qk_hook);
+  fwd2_softmax<E, DP, BK>(st, s, pb, t, mask_tile, qi, p, c, wsz, hh);
+  fwd2_pv<E, DP, BK, TU>(vt, trb, pb, st);
 }
 
 // Q fragments of the lane's query row, pre-scaled by c (rounded to the element type) on the
@@ -376,6 +397,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
 // partial softmax states (O, m, l) merge through LDS before group 0 stores the block.
 // NWG = 4: one 512-thread workgroup per CU; NWG = 2 (64-row blocks, BK = 32): two
 // independent 256-thread workgroups per CU, whose waves are not tied by a shared barrier.
+
 template <class E, int DP, int BK, int NWG>
 __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p) {
   constexpr int NT = NWG * 64, BQ = NWG * 32, ND = DP / 32;
@@ -449,6 +471,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
       __syncthreads();
       cur ^= 1;
     }
+
 
     MFA_STAMP(2 + 3 * which);
     // Merge group 1's partial state into group 0 through LDS (the staging ring is free).
