@@ -38,6 +38,15 @@ __device__ unsigned long long g_mfa_stamps[1 << 20];
       g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (slot)] = t_; \
   } while (0)
 #define MFA_STAMP_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+// Shader-cycle counter at the kernel's start (slot 0) and end (slot 1) of each wave: with the
+// s_memrealtime stamps this gives the clock the chip held during the kernel.
+__device__ unsigned long long g_mfa_cyc[1 << 18];
+#define MFA_CYC(slot)                                                                        \
+  do {                                                                                       \
+    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                              \
+    if ((threadIdx.x & 63) == 0)                                                             \
+      g_mfa_cyc[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (slot)] = c_; \
+  } while (0)
 // Shader-cycle phase totals (slots 5..7 of the wave's record).
 #define MFA_ACC_DECL() unsigned long long acc_[3] = {0, 0, 0}, acct_ = __builtin_amdgcn_s_memtime()
 #define MFA_ACC(k)                                                  \
@@ -53,6 +62,7 @@ __device__ unsigned long long g_mfa_stamps[1 << 20];
         g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 5 + k_] = acc_[k_]; \
   } while (0)
 #else
+#define MFA_CYC(slot) do {} while (0)
 #define MFA_ACC_DECL() do {} while (0)
 #define MFA_ACC(k) do {} while (0)
 #define MFA_ACC_END() do {} while (0)
@@ -324,6 +334,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   const int rb = p.nblk - 1 - blk;
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   MFA_STAMP(0);
+  MFA_CYC(0);
   const int q0 = rb * BQ;
   const int qi = q0 + wave * 32 + l32;
   const bool qvalid = qi < p.R;
@@ -386,6 +397,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   if (!(l > 0.f)) l = kFltMin;
   if (qvalid) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
   MFA_STAMP(3);
+  MFA_CYC(1);
   MFA_STAMP_DRAIN();
   MFA_STAMP(4);
 }
@@ -422,6 +434,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
   const float c = p.c_log2;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
   MFA_STAMP(0);
+  MFA_CYC(0);
 
   DmaA<DP, BK, NT> kd, vd;
   kd.init((int)p.k.ss * 2, p.C, p.D * 2, gt);
@@ -535,6 +548,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
     __syncthreads();
     MFA_STAMP(3 + 3 * which);
   }
+  MFA_CYC(1);
   MFA_STAMP_DRAIN();
   MFA_STAMP(7);
 }

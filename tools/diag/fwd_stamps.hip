@@ -4,6 +4,7 @@
 // Prints, per stamp slot, the spread over waves of (slot time − kernel's first start), µs.
 #define MFA_STAMPS 1
 #include "../../metal-flash-attention-plus_amd/csrc/attention_fwd_v2.hip"
+#include "../../metal-flash-attention-plus_amd/csrc/attention_fwd_v3.hip"  // fwd3_dispatch
 
 #include <algorithm>
 #include <cstring>
@@ -126,6 +127,26 @@ int main(int argc, char** argv) {
   CK(mfa::fwd2_dispatch(p, mfa::P_FP16, D, st));
   CK(hipStreamSynchronize(st));
   CK(hipMemcpy(stamps.data(), dsym, sizeof(unsigned long long) << 20, hipMemcpyDeviceToHost));
+  {
+    // Held clock: shader cycles over s_memrealtime (100 MHz) between each wave's first and
+    // last stamp, median over waves (MI355X_MICROARCH.md, DVFS item 6).
+    std::vector<unsigned long long> cyc(1 << 18, 0);
+    void* csym;
+    CK(hipGetSymbolAddress(&csym, HIP_SYMBOL(mfa::g_mfa_cyc)));
+    CK(hipMemcpy(cyc.data(), csym, sizeof(unsigned long long) << 18, hipMemcpyDeviceToHost));
+    const int last = (var[0] == 'p') ? 7 : 4;
+    std::vector<double> mhz;
+    for (int w = 0; w < (1 << 17); ++w) {
+      const unsigned long long r0 = stamps[w * 8], r1 = stamps[w * 8 + last];
+      if (!r0 || !r1 || r1 <= r0 || !cyc[2 * w] || !cyc[2 * w + 1]) continue;
+      mhz.push_back((double)(cyc[2 * w + 1] - cyc[2 * w]) / ((double)(r1 - r0) / 100.0));
+    }
+    if (!mhz.empty()) {
+      std::sort(mhz.begin(), mhz.end());
+      printf("held clock: median %.0f MHz (p10 %.0f, p90 %.0f, %zu waves)\n", mhz[mhz.size() / 2],
+             mhz[mhz.size() / 10], mhz[mhz.size() * 9 / 10], mhz.size());
+    }
+  }
   unsigned long long t0 = ~0ull, tend = 0;
   int nw = 0;
   for (int w = 0; w < (1 << 17); ++w) {
