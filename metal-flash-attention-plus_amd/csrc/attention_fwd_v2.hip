@@ -245,9 +245,11 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
 
 // Q fragments of the lane's query row, pre-scaled by c (rounded to the element type) on the
 // fp16 path.
-template <class E, int DP>
-__device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p, int b, int h,
-                                        int qi, bool qvalid, int hh, float c) {
+// Q fragments in two halves so a caller can issue the loads early and scale them later
+// (the pair kernel overlaps the next block's Q with the current block's merge and stores).
+template <int DP>
+__device__ __forceinline__ void load_q2_raw(i16x8 (&qf)[DP / 16], const FwdParams& p, int b,
+                                            int h, int qi, bool qvalid, int hh) {
   const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh +
                          (int64_t)(qvalid ? qi : 0) * p.q.ss;
 #pragma unroll
@@ -255,12 +257,25 @@ __device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p
     const int d0 = 16 * s + 8 * hh;
     i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (qvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-    if constexpr (E::prec == P_FP16 && DP <= 128) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (short)E::from_f32(E::to_f32((uint16_t)v[j]) * c);
-    }
     qf[s] = v;
   }
+}
+
+template <class E, int DP>
+__device__ __forceinline__ void prescale_q2(i16x8 (&qf)[DP / 16], float c) {
+  if constexpr (E::prec == P_FP16 && DP <= 128) {
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (short)E::from_f32(E::to_f32((uint16_t)qf[s][j]) * c);
+  }
+}
+
+template <class E, int DP>
+__device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p, int b, int h,
+                                        int qi, bool qvalid, int hh, float c) {
+  load_q2_raw<DP>(qf, p, b, h, qi, qvalid, hh);
+  prescale_q2<E, DP>(qf, c);
 }
 
 __device__ __forceinline__ void store_l(const FwdParams& p, float L, int b, int h, int qi) {
@@ -410,10 +425,17 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
 // NWG = 4: one 512-thread workgroup per CU; NWG = 2 (64-row blocks, BK = 32): two
 // independent 256-thread workgroups per CU, whose waves are not tied by a shared barrier.
 
-template <class E, int DP, int BK, int NWG>
+// OVL: the seam between the two blocks overlaps.  The staging ring is laid out slot-major
+// (slot 0 of both groups in [0, 4*TILEB), slot 1 in [4*TILEB, 8*TILEB)), so once the first
+// block's loop ends, the second block's first K/V tiles and its Q fragments are issued into
+// slot 0 and registers before the merge, which runs over slot 1 and beyond; block two then
+// waits with a counted vmcnt that leaves block one's O stores in flight.
+template <class E, int DP, int BK, int NWG, bool OVL>
 __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p) {
   constexpr int NT = NWG * 64, BQ = NWG * 32, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
+  constexpr int CPR = DP / 4;                        // 16-byte O chunks per row
+  constexpr int OST = BQ * CPR / (2 * NT);           // O stores per thread per block
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -423,8 +445,11 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
   const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
-  char* const kb0 = smem + g * 4 * TILEB;
-  char* const vb0 = kb0 + 2 * TILEB;
+  // K of ring slot s at kb0 + s * SLOT, V at vb0 + s * SLOT.
+  constexpr int SLOT = OVL ? 4 * TILEB : TILEB;
+  char* const kb0 = smem + (OVL ? g * 2 * TILEB : g * 4 * TILEB);
+  char* const vb0 = kb0 + (OVL ? TILEB : 2 * TILEB);
+  char* const mbase = smem + (OVL ? 4 * TILEB : 0);  // merge area / O row image
 
   const int BH = p.B * p.H;
   const int bid = blockIdx.x;
@@ -442,29 +467,47 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
   const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
   const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
 
+  // This group's key range [t0, t1) of query block rb and the shared step count nA.
+  auto range = [&](int rb, int& t0, int& t1, int& nA) {
+    int kbeg, kend;
+    key_range(p, rb * BQ, BQ, BK, &kbeg, &kend);
+    const int ntile = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    nA = (ntile + 1) / 2;
+    t0 = g == 0 ? kbeg : kbeg + nA * BK;
+    t1 = g == 0 ? min(kend, kbeg + nA * BK) : kend;
+  };
+
   const int rbA = pi, rbB = p.nblk - 1 - pi;
+  i16x8 qf[DP / 16];
+  int t0, t1, nA;
+  range(rbB, t0, t1, nA);
+  if (t0 < t1) {
+    kd.issue(khead, t0, kb0);
+    vd.issue(vhead, t0, vb0);
+  }
+  load_q2_raw<DP>(qf, p, b, h, rbB * BQ + wg * 32 + l32, rbB * BQ + wg * 32 + l32 < p.R, hh);
+  bool counted = false;  // this block's loads were issued before the previous block's stores
   for (int which = 0; which < 2; ++which) {
     const int rb = which == 0 ? rbB : rbA;
     if (which == 1 && rbA >= rbB) break;  // odd middle block handled once
     const int q0 = rb * BQ;
     const int qi = q0 + wg * 32 + l32;
     const bool qvalid = qi < p.R;
-    int kbeg, kend;
-    key_range(p, q0, BQ, BK, &kbeg, &kend);
-    const int ntile = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-    const int nA = (ntile + 1) / 2;
-    const int t0 = g == 0 ? kbeg : kbeg + nA * BK;
-    const int t1 = g == 0 ? min(kend, kbeg + nA * BK) : kend;
-
-    if (t0 < t1) {
-      kd.issue(khead, t0, kb0);
-      vd.issue(vhead, t0, vb0);
+    if (!OVL && which == 1) {
+      if (t0 < t1) {
+        kd.issue(khead, t0, kb0);
+        vd.issue(vhead, t0, vb0);
+      }
+      load_q2_raw<DP>(qf, p, b, h, qi, qvalid, hh);
     }
-    i16x8 qf[DP / 16];
-    load_q2<E, DP>(qf, p, b, h, qi, qvalid, hh, c);
+    // Older than the (at most OST + 1) stores the previous block left in flight.
+    if (OVL && counted)
+      __builtin_amdgcn_s_waitcnt(0x0F70 | (OST & 15) | ((OST >> 4) << 14));
+    else
+      wait_vm();
+    prescale_q2<E, DP>(qf, c);
     RowState<DP> st;
     st.init();
-    wait_vm();
     __syncthreads();
     MFA_STAMP(1 + 3 * which);
     int cur = 0;
@@ -472,12 +515,12 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
       const int t = t0 + step * BK;
       if (t < t1) {
         if (t + BK < t1) {
-          kd.issue(khead, t + BK, kb0 + (cur ^ 1) * TILEB);
-          vd.issue(vhead, t + BK, vb0 + (cur ^ 1) * TILEB);
+          kd.issue(khead, t + BK, kb0 + (cur ^ 1) * SLOT);
+          vd.issue(vhead, t + BK, vb0 + (cur ^ 1) * SLOT);
         }
         const bool mask_tile =
             (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
-        fwd2_tile<E, DP, BK>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t,
+        fwd2_tile<E, DP, BK>(kb0 + cur * SLOT, vb0 + cur * SLOT, rbase, trb, qf, st, t,
                              mask_tile, qi, p, c, wsz, hh);
         wait_vm();
       }
@@ -485,10 +528,25 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
       cur ^= 1;
     }
 
-
     MFA_STAMP(2 + 3 * which);
-    // Merge group 1's partial state into group 0 through LDS (the staging ring is free).
-    float* mrg = reinterpret_cast<float*>(smem);        // [NWG waves][ND*16][64]
+    if (which == 0) {
+      range(rbA, t0, t1, nA);
+      if (OVL && rbA < rbB) {
+        // Every wave passed the loop's last barrier: slot 0 is free for the next block.
+        if (t0 < t1) {
+          kd.issue(khead, t0, kb0);
+          vd.issue(vhead, t0, vb0);
+        }
+        const int nqi = rbA * BQ + wg * 32 + l32;
+        load_q2_raw<DP>(qf, p, b, h, nqi, nqi < p.R, hh);
+        // Full block: every wave issues exactly OST O stores after these loads (and group 0
+        // one L store before them), so a counted wait covers the loads.
+        counted = q0 + BQ <= p.R && p.D == DP;
+        __asm__ __volatile__("" ::: "memory");  // keep the loads ahead of the stores
+      }
+    }
+    // Merge group 1's partial state into group 0 through LDS.
+    float* mrg = reinterpret_cast<float*>(mbase);       // [NWG waves][ND*16][64]
     float* mml = mrg + NWG * ND * 16 * 64;              // [NWG waves][2][64]
     if (g == 1) {
 #pragma unroll
@@ -523,7 +581,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
     // instead of 64 rows x 16 B.
     constexpr int ORS = DP * 4 + 16;  // padded row stride (bytes): conflict-free b128 writes
     if (g == 0) {
-      char* orow = smem + (wg * 32 + l32) * ORS;
+      char* orow = mbase + (wg * 32 + l32) * ORS;
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -534,15 +592,14 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
     }
     __syncthreads();
     {
-      constexpr int CPR = DP / 4;  // 16-byte chunks per row
       float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
 #pragma unroll
-      for (int k = 0; k < BQ * CPR / (2 * NT); ++k) {
+      for (int k = 0; k < OST; ++k) {
         const int idx = k * 2 * NT + tid;
         const int r = idx / CPR, d = (idx % CPR) * 4;
         if (q0 + r < p.R && d < p.D)
           *reinterpret_cast<float4*>(obase + (int64_t)(q0 + r) * p.o_ss + d) =
-              *reinterpret_cast<const float4*>(smem + r * ORS + d * 4);
+              *reinterpret_cast<const float4*>(mbase + r * ORS + d * 4);
       }
     }
     __syncthreads();
@@ -560,12 +617,18 @@ static hipError_t launch_fwd2(const FwdParams& p, hipStream_t stream) {
   return launch(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
 }
 
-template <class E, int DP, int BK, int NWG>
+template <class E, int DP, int BK, int NWG, bool OVL = true>
 static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
-  constexpr int LDS = 8 * BK * DP * 2;
-  static_assert(LDS >= NWG * (DP / 32) * 16 * 64 * 4 + NWG * 2 * 64 * 4, "merge area");
-  static_assert(LDS >= NWG * 32 * (DP * 4 + 16), "O row image");
-  auto kern = mfa_fwd2_pair_kernel<E, DP, BK, NWG>;
+  constexpr int MERGE = NWG * (DP / 32) * 16 * 64 * 4 + NWG * 2 * 64 * 4;
+  constexpr int OIMG = NWG * 32 * (DP * 4 + 16);
+  constexpr int MB = OVL ? 4 * BK * DP * 2 : 0;  // merge area / O image base
+  constexpr int RING = 8 * BK * DP * 2;
+  constexpr int LDS = RING > MB + MERGE && RING > MB + OIMG ? RING
+                      : (MERGE > OIMG ? MB + MERGE : MB + OIMG);
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(NWG * 32 * (DP / 4) % (NWG * 128) == 0 && NWG * 32 * (DP / 4) / (NWG * 128) < 64,
+                "O stores per thread (counted vmcnt)");
+  auto kern = mfa_fwd2_pair_kernel<E, DP, BK, NWG, OVL>;
   FwdParams q = p;
   q.nblk = (p.R + NWG * 32 - 1) / (NWG * 32);
   const int npairs = (q.nblk + 1) / 2;
@@ -599,6 +662,8 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   }
   const char* pv = getenv("MFA_FWD_PAIR");
   const bool pair64 = pv && pv[0] == '2';
+  if (pv && pv[0] == 'n' && elem == P_FP16 && DP == 128 && !single)  // A/B: serial seam
+    return launch_fwd2_pair<F16, 128, 64, 4, false>(p, stream);
 #define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                          \
   if (elem == ELEM && DP == DPV)                                                \
     return single ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)                   \
@@ -616,13 +681,14 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
 
 #define MFA_F2_INST(EE, DPV, BKV, WPS)                                        \
   template __global__ void mfa_fwd2_kernel<EE, DPV, BKV, WPS>(FwdParams);     \
-  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV, 4>(FwdParams);  \
-  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, 32, 2>(FwdParams);
+  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV, 4, true>(FwdParams);  \
+  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, 32, 2, true>(FwdParams);
 MFA_F2_INST(F16, 64, 64, 2)
 MFA_F2_INST(F16, 128, 64, 2)
 MFA_F2_INST(BF16, 64, 64, 2)
 MFA_F2_INST(BF16, 128, 64, 2)
 #undef MFA_F2_INST
+template __global__ void mfa_fwd2_pair_kernel<F16, 128, 64, 4, false>(FwdParams);
 template __global__ void mfa_fwd2_kernel<F16, 256, 32, 2>(FwdParams);
 template __global__ void mfa_fwd2_kernel<BF16, 256, 32, 2>(FwdParams);
 

@@ -354,8 +354,10 @@ __device__ __forceinline__ void lds_dma16(const void* base, int nrec, int voff, 
   rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);
   rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
   rs[3] = 0x00020000u;
-  const unsigned lds = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)dst));
+  // The low 32 bits of a generic LDS pointer are its LDS address; an explicit address-space
+  // cast here can make the selector emit a null check on the shared aperture it then fails
+  // to encode ("V_CMP_NE_U32 0, $src_shared_base").
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
   asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                :
                : "v"(voff), "s"(rs), "s"(lds)

@@ -25,8 +25,8 @@ def one(plan):
 # C5 B8 H32 S4096 D256 fwd + bwd.
 def test_c2_headline_runs_mirrored_pair_kernel():
     p = one(mfa.multihead_plan(mh(1, 16, 4096, 128, causal=True)))
-    assert p["name"] == "mfa_fwd2_pair_kernel<F16, 128, 64, 4>"
-    assert p["threads"] == 512 and p["lds_bytes"] == 128 * 1024
+    assert p["name"] == "mfa_fwd2_pair_kernel<F16, 128, 64, 4, true>"
+    assert p["threads"] == 512 and p["lds_bytes"] == 64 * 1024 + 128 * 528  # ring + O image
     # 32 query blocks of 128 rows per head, mirrored in pairs: 16 x 16 heads.
     assert p["workgroups"] == 16 * 16
 
@@ -54,7 +54,7 @@ def test_bf16_and_d64_instantiations():
     assert one(mfa.multihead_plan(mh(1, 4, 1024, 128, prec=P.BF16)))["name"].startswith(
         "mfa_fwd2_kernel<BF16, 128")
     assert one(mfa.multihead_plan(mh(1, 16, 4096, 64, causal=True)))["name"] == \
-        "mfa_fwd2_pair_kernel<F16, 64, 64, 4>"
+        "mfa_fwd2_pair_kernel<F16, 64, 64, 4, true>"
 
 
 def test_fp32_inputs_take_generic_kernel():
