@@ -481,13 +481,11 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
   i16x8 qf[DP / 16];
   int t0, t1, nA;
   range(rbB, t0, t1, nA);
-  // Prologue in the order the first tile consumes it: K and Q, then V, which is waited for
-  // only before the first PV (a third of the prologue burst overlaps QK^T and softmax).
-  if (t0 < t1) kd.issue(khead, t0, kb0);
+  if (t0 < t1) {
+    kd.issue(khead, t0, kb0);
+    vd.issue(vhead, t0, vb0);
+  }
   load_q2_raw<DP>(qf, p, b, h, rbB * BQ + wg * 32 + l32, rbB * BQ + wg * 32 + l32 < p.R, hh);
-  __asm__ __volatile__("" ::: "memory");
-  if (t0 < t1) vd.issue(vhead, t0, vb0);
-  constexpr int PPW = DmaA<DP, BK, NT>::PPW;
   bool counted = false;  // this block's loads were issued before the previous block's stores
   for (int which = 0; which < 2; ++which) {
     const int rb = which == 0 ? rbB : rbA;
@@ -505,8 +503,6 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
     // Older than the (at most OST + 1) stores the previous block left in flight.
     if (OVL && counted)
       __builtin_amdgcn_s_waitcnt(0x0F70 | (OST & 15) | ((OST >> 4) << 14));
-    else if (OVL && which == 0 && t0 < t1)
-      __builtin_amdgcn_s_waitcnt(0x0F70 | PPW);  // K and Q; V may be in flight
     else
       wait_vm();
     prescale_q2<E, DP>(qf, c);
@@ -515,37 +511,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
     __syncthreads();
     MFA_STAMP(1 + 3 * which);
     int cur = 0;
-    int step = 0;
-    if (OVL && which == 0) {
-      // First tile: PV waits (counted, then a barrier every wave reaches) for the V tile.
-      const int t = t0;
-      const bool act = t < t1, nxt = t + BK < t1;
-      f32x16 s[BK / 32];
-      i16x8 pb[BK / 16];
-      if (act) {
-        if (nxt) {
-          kd.issue(khead, t + BK, kb0 + SLOT);
-          vd.issue(vhead, t + BK, vb0 + SLOT);
-        }
-        const bool mask_tile =
-            (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
-        fwd2_qk<E, DP, BK, TuneDefault>(kb0, rbase, qf, st, s, NoHook());
-        fwd2_softmax<E, DP, BK>(st, s, pb, t, mask_tile, qi, p, c, wsz, hh);
-      }
-      if (act && nxt)
-        __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * PPW));
-      else
-        wait_vm();
-      __syncthreads();
-      if (act) {
-        fwd2_pv<E, DP, BK, TuneDefault>(vb0, trb, pb, st);
-        wait_vm();
-      }
-      __syncthreads();
-      cur = 1;
-      step = 1;
-    }
-    for (; step < nA; ++step) {
+    for (int step = 0; step < nA; ++step) {
       const int t = t0 + step * BK;
       if (t < t1) {
         if (t + BK < t1) {
