@@ -1,0 +1,65 @@
+"""CPU check of the built library's code-object metadata: the kernels the dispatcher launches
+for the BASELINE configurations (and the quantised / MLA / GEMM rows beside them) use no
+scratch memory, i.e. no register spills to HBM, and fit the register file.  A spill here is
+silent on the GPU (results stay correct) and shows up only as extra HBM traffic in the
+PMC passes; this pins it at build time.  Needs the ROCm LLVM tools (present
+in this image); skipped otherwise."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = os.path.join(_REPO, "metal-flash-attention-plus_amd", "libmfa_amd.so")
+_LLVM = "/opt/rocm/lib/llvm/bin"
+
+# Mangled-name fragments of the tuned kernels (csrc/attention_fwd_v2.hip, attention_fwd_i8.hip,
+# attention_bwd_fast.hip, attention_mla_latent.hip, kv_dequant.hip, gemm.hip, quantize.hip).
+HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd_i8_kernel", "mfa_bwd_q_fast_kernel",
+       "mfa_bwd_kv_fast_kernel", "mfa_mla", "mfa_kv_dequant_kernel", "mfa_gemm2_kernel",
+       "qz_")
+
+
+@pytest.fixture(scope="module")
+def kernels(tmp_path_factory):
+    if not (os.path.exists(_LIB) and os.path.exists(os.path.join(_LLVM, "llvm-readelf"))):
+        pytest.skip("library or ROCm LLVM tools not present")
+    d = tmp_path_factory.mktemp("co")
+    lib = shutil.copy(_LIB, d)
+    subprocess.run([os.path.join(_LLVM, "llvm-objdump"), "--offloading", lib], check=True,
+                   capture_output=True, cwd=d)
+    notes = ""
+    for f in sorted(os.listdir(d)):
+        if f.endswith("gfx950"):
+            notes += subprocess.run([os.path.join(_LLVM, "llvm-readelf"), "--notes",
+                                     os.path.join(d, f)], check=True, capture_output=True,
+                                    text=True).stdout
+    out = {}
+    for ent in notes.split("- .agpr_count")[1:]:
+        def field(k):
+            m = re.search(r"\." + k + r":\s+(\S+)", ent)
+            return m.group(1) if m else None
+        out[field("name")] = {"scratch": int(field("private_segment_fixed_size")),
+                              "vgpr_spill": int(field("vgpr_spill_count")),
+                              "vgpr": int(field("vgpr_count"))}
+    assert out, "no kernel metadata found"
+    return out
+
+
+def test_hot_kernels_present(kernels):
+    for frag in HOT:
+        assert any(frag in n for n in kernels), frag
+
+
+def test_hot_kernels_use_no_scratch(kernels):
+    bad = {n: k for n, k in kernels.items()
+           if any(f in n for f in HOT) and k["scratch"] != 0}
+    assert not bad, bad
+
+
+def test_hot_kernels_fit_register_file(kernels):
+    for n, k in kernels.items():
+        if any(f in n for f in HOT):
+            assert k["vgpr"] <= 512, (n, k)
