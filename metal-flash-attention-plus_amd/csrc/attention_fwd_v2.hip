@@ -610,6 +610,232 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
   MFA_STAMP(7);
 }
 
+// ---------------------------------------------------------------------------------------
+// Causal balance with shared K/V tiles ("share" schedule, no window).  The workgroup owns the
+// mirrored pair of 128-row blocks A (light, pi: nA key tiles) and B (heavy, nblk-1-pi: nB
+// tiles).  A's keys are the first nA of B's, so:
+//   phase 1 (steps 0..nA-1): one tile per step, staged by all 8 waves and read by both
+//     groups — group 0 (waves 0-3) with A's rows, group 1 (waves 4-7) with B's rows.  Half
+//     the K/V bytes and DMA instructions of the pair kernel for these steps;
+//   phase 2: B's remaining nB - nA tiles, split between the groups (each with its own ring,
+//     one tile each per step, as in the pair kernel).  Group 0 enters it with B's rows: it
+//     stores A's O and L from registers at the switch and takes B's Q from LDS, where it
+//     staged them by DMA during the last shared step.
+// Steps: nA + ceil((nB - nA) / 2) — 33 for every workgroup at C2, as in the pair kernel.  B's
+// two partial states merge through LDS at the end.  LDS: ring 0 (shared, then group 0's),
+// ring 1 (group 1's), group 0's Q staging: 160 KiB at D = 128.
+// MIRROR = false (no mask): the pair is two adjacent blocks (2·pi, 2·pi + 1) with the same key
+// range, so every step is a shared one (256 query rows per K/V tile).
+template <class E, int DP, int BK, bool MIRROR>
+__global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
+  constexpr int NT = 256, BQ = 128, ND = DP / 32;
+  constexpr int TILEB = BK * DP * 2;
+  constexpr int QW = 32 * DP * 2;                    // one wave's 32 Q rows
+  constexpr int CPR = DP / 4;                        // 16-byte O chunks per row
+  constexpr int OST = BQ * CPR / (2 * NT);           // O stores per thread (final block)
+  constexpr int NSW = 4 * ND + 1;                    // stores per wave at the switch (O + L)
+  static_assert(NSW < 64, "counted vmcnt");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int g = __builtin_amdgcn_readfirstlane(tid / NT);
+  const int gt = tid % NT;
+  const int lane = tid & 63, wg = gt >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
+  const int trb[2] = {TileA<DP>::tr_base(lane, 0), TileA<DP>::tr_base(lane, 1)};
+  char* const sk = smem;                  // ring 0: K slots 0, 1, then V slots 0, 1
+  char* const sv = smem + 2 * TILEB;
+  char* const kb0 = smem + g * 4 * TILEB; // this group's ring in phase 2
+  char* const vb0 = kb0 + 2 * TILEB;
+  char* const qstg = smem + 8 * TILEB + wg * QW;
+
+  const int BH = p.B * p.H;
+  const int pi = blockIdx.x / BH;
+  const int bh = blockIdx.x % BH;
+  const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
+  const float c = p.c_log2;
+  const int wsz = 0x3fffffff;
+
+  DmaA<DP, BK, NT> kd, vd;         // a group's own tiles
+  DmaA<DP, BK, 2 * NT> ksh, vsh;   // shared tiles, staged by all 8 waves
+  kd.init((int)p.k.ss * 2, p.C, p.D * 2, gt);
+  vd.init((int)p.v.ss * 2, p.C, p.D * 2, gt);
+  ksh.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
+  vsh.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
+  const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
+  const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
+
+  const int rbA = MIRROR ? pi : 2 * pi;
+  const int rbB = MIRROR ? p.nblk - 1 - pi : min(2 * pi + 1, p.nblk - 1);
+  int a0, a1, b0, b1;
+  key_range(p, rbA * BQ, BQ, BK, &a0, &a1);
+  key_range(p, rbB * BQ, BQ, BK, &b0, &b1);
+  const int nA = rbA < rbB && a1 > a0 ? (a1 - a0 + BK - 1) / BK : 0;  // odd last block: B only
+  const int nB = b1 > b0 ? (b1 - b0 + BK - 1) / BK : 0;
+  const int n2 = nB - nA;            // phase-2 tiles
+  const int h0 = (n2 + 1) / 2;       // group 0's share of them
+  const int S = nA + h0;
+  // Tile index of this group at step s (group 0: s; group 1: s, then s + h0); false past its
+  // range.
+  auto tile = [&](int s, int& t) -> bool {
+    const int i = (g == 1 && s >= nA) ? s + h0 : s;
+    t = b0 + i * BK;
+    return s < S && i < nB;
+  };
+
+  if (nA > 0) {
+    ksh.issue(khead, b0, sk);
+    vsh.issue(vhead, b0, sv);
+  } else {
+    int t;
+    if (tile(0, t)) {
+      kd.issue(khead, t, kb0);
+      vd.issue(vhead, t, vb0);
+    }
+  }
+  int q0 = (g == 0 && nA > 0 ? rbA : rbB) * BQ;
+  int qi = q0 + wg * 32 + l32;
+  i16x8 qf[DP / 16];
+  load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
+  DmaA<DP, 32, 64> qd;  // group 0: B's Q rows of this wave, staged for the switch
+  qd.init((int)p.q.ss * 2, p.R, p.D * 2, lane);
+  const char* qhead = (const char*)p.q.ptr + ((int64_t)b * p.q.sb + (int64_t)h * p.q.sh) * 2;
+  RowState<DP> st;
+  st.init();
+  wait_vm();
+  prescale_q2<E, DP>(qf, c);
+  __syncthreads();
+
+  const bool full_sw = rbA * BQ + BQ <= p.R && p.D == DP;  // every switch store is issued
+  auto step = [&](int s, bool sw) {
+    // Stage the next step's tile(s) into the slot read two steps ago.
+    const int nx = (s + 1) & 1;
+    if (s + 1 < nA) {
+      ksh.issue(khead, b0 + (s + 1) * BK, sk + nx * TILEB);
+      vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
+    } else {
+      int tn;
+      if (tile(s + 1, tn)) {
+        kd.issue(khead, tn, kb0 + nx * TILEB);
+        vd.issue(vhead, tn, vb0 + nx * TILEB);
+      }
+    }
+    if (sw) {
+      // A is complete: its O and L leave from registers (the next tiles' DMA is older than
+      // these stores, so the step's counted wait below leaves them in flight).
+      float l = cross_half_sum(st.lh) + kFltMin;
+      if (!(l > 0.f)) l = kFltMin;
+      if (qi < p.R) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+      __asm__ __volatile__("" ::: "memory");
+      q0 = rbB * BQ;
+      qi = q0 + wg * 32 + l32;
+      using A = Arith16<E, DP>;
+#pragma unroll
+      for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(qstg, rbase, 0, ds);
+      prescale_q2<E, DP>(qf, c);
+      st.init();
+    }
+    int tc;
+    if (tile(s, tc)) {
+      const bool shared = s < nA;
+      const char* kt = (shared ? sk : kb0) + (s & 1) * TILEB;
+      const char* vt = (shared ? sv : vb0) + (s & 1) * TILEB;
+      const bool mask_tile = (tc + BK > p.C) || (p.mask.causal && tc + BK - 1 > q0);
+      fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh);
+    }
+    if (sw && full_sw)
+      __builtin_amdgcn_s_waitcnt(0x0F70 | (NSW & 15) | ((NSW >> 4) << 14));
+    else
+      wait_vm();
+    __syncthreads();
+  };
+  // Phase 1 up to its last step, which also stages B's Q rows; group 0 switches at step nA.
+  int s = 0;
+  for (; s < nA - 1; ++s) step(s, false);
+  if (nA > 0 && n2 > 0) {
+    if (g == 0) qd.issue(qhead, rbB * BQ + wg * 32, qstg);
+    step(s++, false);
+    step(s++, g == 0);
+  }
+  for (; s < S; ++s) step(s, false);
+
+  char* const mbase = smem;  // the rings are free: merge area, then the O row image
+  if (n2 == 0) {
+    // Group 0 holds all of A (if any), group 1 all of B: no merge.
+    float l = cross_half_sum(st.lh) + kFltMin;
+    if (!(l > 0.f)) l = kFltMin;
+    if (qi < p.R && (g == 1 || nA > 0)) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+    return;
+  }
+  // Merge group 1's partial state of B into group 0 through LDS.
+  float* mrg = reinterpret_cast<float*>(mbase);       // [4 waves][ND*16][64]
+  float* mml = mrg + 4 * ND * 16 * 64;                // [4 waves][2][64]
+  if (g == 1) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mrg[((wg * ND + dt) * 16 + i) * 64 + lane] = st.o[dt][i];
+    mml[(wg * 2 + 0) * 64 + lane] = st.m;
+    mml[(wg * 2 + 1) * 64 + lane] = st.lh;
+  }
+  __syncthreads();
+  float inv = 0.f;
+  if (g == 0) {
+    const float mb = mml[(wg * 2 + 0) * 64 + lane];
+    const float lb = mml[(wg * 2 + 1) * 64 + lane];
+    const float mf = fmaxf(st.m, mb);
+    const float ca = __builtin_amdgcn_exp2f(st.m - mf);
+    const float cb = __builtin_amdgcn_exp2f(mb - mf);
+    float l = cross_half_sum(st.lh * ca + lb * cb) + kFltMin;
+    if (!(l > 0.f)) l = kFltMin;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        st.o[dt][i] = st.o[dt][i] * ca + mrg[((wg * ND + dt) * 16 + i) * 64 + lane] * cb;
+    inv = p.o_mul / l;
+    if (hh == 0 && qi < p.R) store_l(p, mf + __log2f(l), b, h, qi);
+  }
+  __syncthreads();
+  // O leaves through LDS as whole rows (T21), as in the pair kernel.
+  constexpr int ORS = DP * 4 + 16;
+  if (g == 0) {
+    char* orow = mbase + (wg * 32 + l32) * ORS;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+        *reinterpret_cast<float4*>(orow + (dt * 32 + 8 * gq + 4 * hh) * 4) =
+            make_float4(st.o[dt][4 * gq] * inv, st.o[dt][4 * gq + 1] * inv,
+                        st.o[dt][4 * gq + 2] * inv, st.o[dt][4 * gq + 3] * inv);
+  }
+  __syncthreads();
+  float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+#pragma unroll
+  for (int k = 0; k < OST; ++k) {
+    const int idx = k * 2 * NT + tid;
+    const int r = idx / CPR, d = (idx % CPR) * 4;
+    if (q0 + r < p.R && d < p.D)
+      *reinterpret_cast<float4*>(obase + (int64_t)(q0 + r) * p.o_ss + d) =
+          *reinterpret_cast<const float4*>(mbase + r * ORS + d * 4);
+  }
+}
+
+template <class E, int DP, int BK, bool MIRROR = true>
+static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
+  constexpr int RING = 8 * BK * DP * 2 + 4 * 32 * DP * 2;
+  constexpr int MERGE = 4 * (DP / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4;
+  constexpr int OIMG = 128 * (DP * 4 + 16);
+  constexpr int LDS = RING > MERGE ? (RING > OIMG ? RING : OIMG) : (MERGE > OIMG ? MERGE : OIMG);
+  static_assert(LDS <= 160 * 1024, "LDS");
+  FwdParams q = p;
+  q.nblk = (p.R + 127) / 128;
+  const int npairs = (q.nblk + 1) / 2;
+  return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR>, dim3(npairs * p.B * p.H), dim3(512),
+                LDS, stream, q);
+}
+
 template <class E, int DP, int BK, int WPS, class TU = TuneDefault>
 static hipError_t launch_fwd2(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 4 * BK * DP * 2;
@@ -662,13 +888,24 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   }
   const char* pv = getenv("MFA_FWD_PAIR");
   const bool pair64 = pv && pv[0] == '2';
+  // Causal pairs run the shared-tile schedule; MFA_FWD_PAIR=o keeps the pair kernel (A/B).
+  const bool share = !(pv && (pv[0] == 'o' || pv[0] == '2' || pv[0] == 'n')) && !p.mask.window;
   if (pv && pv[0] == 'n' && elem == P_FP16 && DP == 128 && !single)  // A/B: serial seam
     return launch_fwd2_pair<F16, 128, 64, 4, false>(p, stream);
+  // Unmasked forwards with at least a full wave of pairs: adjacent block pairs share every
+  // K/V tile (256 query rows per staged tile; +6.5 % at C3 over the single-block kernel).
+  // MFA_FWD_SHARE=0 keeps the single-block kernel (A/B).
+  const char* sv = getenv("MFA_FWD_SHARE");
+  const bool adj = !(sv && sv[0] == '0') && !p.mask.causal && !p.mask.window && !var &&
+                   (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256;
 #define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                          \
+  if (elem == ELEM && DP == DPV && adj)                                         \
+    return launch_fwd2_share<EE, DPV, BKV, false>(p, stream);                   \
   if (elem == ELEM && DP == DPV)                                                \
-    return single ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)                   \
-                  : (pair64 ? launch_fwd2_pair<EE, DPV, 32, 2>(p, stream)       \
-                            : launch_fwd2_pair<EE, DPV, BKV, 4>(p, stream));
+    return single  ? launch_fwd2<EE, DPV, BKV, WPS>(p, stream)                  \
+           : share ? launch_fwd2_share<EE, DPV, BKV>(p, stream)                  \
+                   : (pair64 ? launch_fwd2_pair<EE, DPV, 32, 2>(p, stream)       \
+                             : launch_fwd2_pair<EE, DPV, BKV, 4>(p, stream));
   MFA_F2(P_FP16, F16, 64, 64, 2)
   MFA_F2(P_FP16, F16, 128, 64, 2)
   MFA_F2(P_BF16, BF16, 64, 64, 2)
@@ -682,7 +919,9 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
 #define MFA_F2_INST(EE, DPV, BKV, WPS)                                        \
   template __global__ void mfa_fwd2_kernel<EE, DPV, BKV, WPS>(FwdParams);     \
   template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV, 4, true>(FwdParams);  \
-  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, 32, 2, true>(FwdParams);
+  template __global__ void mfa_fwd2_pair_kernel<EE, DPV, 32, 2, true>(FwdParams);  \
+  template __global__ void mfa_fwd2_share_kernel<EE, DPV, BKV, true>(FwdParams);  \
+  template __global__ void mfa_fwd2_share_kernel<EE, DPV, BKV, false>(FwdParams);
 MFA_F2_INST(F16, 64, 64, 2)
 MFA_F2_INST(F16, 128, 64, 2)
 MFA_F2_INST(BF16, 64, 64, 2)

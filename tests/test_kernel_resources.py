@@ -17,7 +17,7 @@ _LLVM = "/opt/rocm/lib/llvm/bin"
 
 # Mangled-name fragments of the tuned kernels (csrc/attention_fwd_v2.hip, attention_fwd_i8.hip,
 # attention_bwd_fast.hip, attention_mla_latent.hip, kv_dequant.hip, gemm.hip, quantize.hip).
-HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd_i8_kernel", "mfa_bwd_q_fast_kernel",
+HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd2_share_kernel", "mfa_fwd_i8_kernel", "mfa_bwd_q_fast_kernel",
        "mfa_bwd_kv_fast_kernel", "mfa_mla", "mfa_kv_dequant_kernel", "mfa_gemm2_kernel",
        "qz_")
 

@@ -23,18 +23,26 @@ def one(plan):
 
 # BASELINE.json configs: C2 (headline) fp16 causal H16 S4096 D128; C3 H16 S8192 non-causal;
 # C5 B8 H32 S4096 D256 fwd + bwd.
-def test_c2_headline_runs_mirrored_pair_kernel():
+def test_c2_headline_runs_shared_tile_pair_kernel():
     p = one(mfa.multihead_plan(mh(1, 16, 4096, 128, causal=True)))
-    assert p["name"] == "mfa_fwd2_pair_kernel<F16, 128, 64, 4, true>"
-    assert p["threads"] == 512 and p["lds_bytes"] == 64 * 1024 + 128 * 528  # ring + O image
+    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, true>"
+    assert p["threads"] == 512 and p["lds_bytes"] == 160 * 1024  # two rings + Q staging
     # 32 query blocks of 128 rows per head, mirrored in pairs: 16 x 16 heads.
     assert p["workgroups"] == 16 * 16
 
 
-def test_c3_runs_single_block_kernel():
+def test_c3_runs_adjacent_shared_tile_kernel():
+    # Unmasked with >= 256 block pairs: adjacent 128-row blocks share every K/V tile.
     p = one(mfa.multihead_plan(mh(1, 16, 8192, 128)))
+    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, false>"
+    assert p["threads"] == 512 and p["workgroups"] == 32 * 16
+
+
+def test_small_unmasked_runs_single_block_kernel():
+    # Fewer than 256 pairs would leave CUs idle: one 4-wave workgroup per 128-row block.
+    p = one(mfa.multihead_plan(mh(1, 16, 2048, 128)))
     assert p["name"].startswith("mfa_fwd2_kernel<F16, 128, 64, 2")
-    assert p["threads"] == 256 and p["workgroups"] == 64 * 16
+    assert p["threads"] == 256 and p["workgroups"] == 16 * 16
 
 
 def test_c5_forward_and_backward_phases():
@@ -54,7 +62,7 @@ def test_bf16_and_d64_instantiations():
     assert one(mfa.multihead_plan(mh(1, 4, 1024, 128, prec=P.BF16)))["name"].startswith(
         "mfa_fwd2_kernel<BF16, 128")
     assert one(mfa.multihead_plan(mh(1, 16, 4096, 64, causal=True)))["name"] == \
-        "mfa_fwd2_pair_kernel<F16, 64, 64, 4, true>"
+        "mfa_fwd2_share_kernel<F16, 64, 64, true>"
 
 
 def test_fp32_inputs_take_generic_kernel():
@@ -84,7 +92,7 @@ def test_quantized_plans():
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(qx)]
     assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
-    assert names[2].startswith("mfa_fwd2_kernel<F16, 128, 64, 2") and len(names) == 3
+    assert names[2] == "mfa_fwd2_share_kernel<F16, 128, 64, false>" and len(names) == 3
     for kind, kern in ((K.backwardQuery, "mfa_bwd_q_fast_kernel<F16, 128, 64>"),
                        (K.backwardKeyValue, "mfa_bwd_kv_fast_kernel<F16, 128, 64>")):
         assert [r["name"] for r in mfa.quantized_plan(qx, kind)][2] == kern
@@ -92,10 +100,10 @@ def test_quantized_plans():
     q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(q4)]
     assert names[:3] == ["mfa_kv_dequant_kernel<F16, 2>"] * 2 + ["mfa_kv_dequant_kernel<F16, 1>"]
-    assert names[3].startswith("mfa_fwd2_kernel<F16, 128")
+    assert names[3] == "mfa_fwd2_share_kernel<F16, 128, 64, false>"
     # A non-zero zero point leaves the integer-matmul kernel (dequant-exact path instead).
     zp = mfa.QuantizedTensor(None, int(P.INT8), 0.5, 3)
-    assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_kernel<")
+    assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_share_kernel<")
     # Decode-like shapes (few query rows per kv head) read the quantised tensors directly.
     dec = mfa.AttentionDescriptor.make(16, 8192, 128, low_precision=True, precision=P.FP16)
     qd = mfa.quantized_descriptor(dec, P.FP16, P.INT8, P.INT8, B=1, H=4)
