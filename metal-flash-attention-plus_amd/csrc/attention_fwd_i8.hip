@@ -38,11 +38,14 @@ __device__ __forceinline__ float xh_sum(float x) {
 
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
-template <class E, int DP, int BK, int OCC>
-__global__ void __launch_bounds__(256, OCC) mfa_fwd_i8_kernel(FwdParams p) {
+// NG = 2 (unmasked forwards): a 512-thread workgroup of two 4-wave groups owns the adjacent
+// 128-row blocks (2·pi, 2·pi + 1), and every K/V tile, staged by all 8 waves, serves both
+// (256 query rows per staged tile, half the LDS-DMA of two 4-wave workgroups).
+template <class E, int DP, int BK, int OCC, int NG = 1>
+__global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) {
   static_assert(DP == 128 && (BK == 64 || BK == 128), "int8 kernel: D<=128, 64/128-key tiles");
   using TK = Tile16<DP / 2>;            // [BK][DP bytes] = 16-byte chunks, DP/16 per row
-  constexpr int NT = 256, BQ = 128;
+  constexpr int NT = 256 * NG, BQ = 128;
   constexpr int NJ = BK / 32;
   constexpr int KSTEPS = DP / 32;       // i8 MFMA k = 32
   constexpr int KTILE = BK * DP;        // bytes
@@ -52,11 +55,12 @@ __global__ void __launch_bounds__(256, OCC) mfa_fwd_i8_kernel(FwdParams p) {
   char* const vb0 = smem + 2 * KTILE;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = (tid & 255) >> 6;
+  const int grp = NG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
   const int l32 = lane & 31, hh = lane >> 5;
   const int BH = p.B * p.H;
   const int bid = blockIdx.x;
-  const int rb = p.nblk - 1 - bid / BH;
+  const int rb = NG > 1 ? NG * (bid / BH) + grp : p.nblk - 1 - bid / BH;
   const int bh = bid % BH;
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const int q0 = rb * BQ;
@@ -309,11 +313,12 @@ __global__ void __launch_bounds__(256, OCC) mfa_fwd_i8_kernel(FwdParams p) {
   }
 }
 
-template <class E, int BK, int OCC>
+template <class E, int BK, int OCC, int NG = 1>
 static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
   constexpr int LDS = 4 * BK * 128;  // K and V, double-buffered
-  auto kern = mfa_fwd_i8_kernel<E, 128, BK, OCC>;
-  return launch(kern, dim3(p.nblk * p.B * p.H), dim3(256), LDS, stream, p);
+  auto kern = mfa_fwd_i8_kernel<E, 128, BK, OCC, NG>;
+  const int units = (p.nblk + NG - 1) / NG;
+  return launch(kern, dim3(units * p.B * p.H), dim3(256 * NG), LDS, stream, p);
 }
 
 // INT8-MFMA forward: Q fp16/bf16 (quantised per row in-kernel), K/V INT8 per-tensor with zero
@@ -323,6 +328,14 @@ static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) {
   const char* bk = getenv("MFA_I8_BK");
   const bool small = bk && bk[0] == '6';
+  // Unmasked, at least a full wave of block pairs: adjacent blocks share the staged tiles
+  // (MFA_I8_SHARE=0 keeps one 4-wave workgroup per block, =1 shares at any size: tests).
+  const char* sh = getenv("MFA_I8_SHARE");
+  if (!small && !p.mask.causal && !p.mask.window &&
+      (sh ? sh[0] == '1' : (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256)) {
+    if (elem == P_FP16) return launch_i8<F16, 128, 2, 2>(p, stream);
+    if (elem == P_BF16) return launch_i8<BF16, 128, 2, 2>(p, stream);
+  }
   if (elem == P_FP16) return small ? launch_i8<F16, 64, 3>(p, stream) : launch_i8<F16, 128, 2>(p, stream);
   if (elem == P_BF16) return small ? launch_i8<BF16, 64, 3>(p, stream) : launch_i8<BF16, 128, 2>(p, stream);
   return hipErrorNotSupported;
@@ -334,5 +347,7 @@ template __global__ void mfa_fwd_i8_kernel<F16, 128, 64, 3>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<BF16, 128, 64, 3>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<F16, 128, 128, 2>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<BF16, 128, 128, 2>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<F16, 128, 128, 2, 2>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<BF16, 128, 128, 2, 2>(FwdParams);
 
 }  // namespace mfa

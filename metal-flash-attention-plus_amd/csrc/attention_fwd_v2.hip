@@ -666,13 +666,15 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
   const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
 
+  // Adjacent pairs: an odd last block leaves group 1 without rows (it still stages tiles).
   const int rbA = MIRROR ? pi : 2 * pi;
-  const int rbB = MIRROR ? p.nblk - 1 - pi : min(2 * pi + 1, p.nblk - 1);
+  const int rbB = MIRROR ? p.nblk - 1 - pi : 2 * pi + 1;
   int a0, a1, b0, b1;
   key_range(p, rbA * BQ, BQ, BK, &a0, &a1);
-  key_range(p, rbB * BQ, BQ, BK, &b0, &b1);
-  const int nA = rbA < rbB && a1 > a0 ? (a1 - a0 + BK - 1) / BK : 0;  // odd last block: B only
+  key_range(p, MIRROR ? rbB * BQ : rbA * BQ, BQ, BK, &b0, &b1);
   const int nB = b1 > b0 ? (b1 - b0 + BK - 1) / BK : 0;
+  // Mirrored: the odd middle block is B only.
+  const int nA = !MIRROR ? nB : rbA < rbB && a1 > a0 ? (a1 - a0 + BK - 1) / BK : 0;
   const int n2 = nB - nA;            // phase-2 tiles
   const int h0 = (n2 + 1) / 2;       // group 0's share of them
   const int S = nA + h0;
@@ -824,10 +826,12 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
 
 template <class E, int DP, int BK, bool MIRROR = true>
 static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
-  constexpr int RING = 8 * BK * DP * 2 + 4 * 32 * DP * 2;
+  // Adjacent pairs use ring 0 only (every step is shared, no merge).
+  constexpr int RING = MIRROR ? 8 * BK * DP * 2 + 4 * 32 * DP * 2 : 4 * BK * DP * 2;
   constexpr int MERGE = 4 * (DP / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4;
   constexpr int OIMG = 128 * (DP * 4 + 16);
-  constexpr int LDS = RING > MERGE ? (RING > OIMG ? RING : OIMG) : (MERGE > OIMG ? MERGE : OIMG);
+  constexpr int LDS = !MIRROR ? RING
+                      : RING > MERGE ? (RING > OIMG ? RING : OIMG) : (MERGE > OIMG ? MERGE : OIMG);
   static_assert(LDS <= 160 * 1024, "LDS");
   FwdParams q = p;
   q.nblk = (p.R + 127) / 128;
@@ -894,10 +898,11 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
     return launch_fwd2_pair<F16, 128, 64, 4, false>(p, stream);
   // Unmasked forwards with at least a full wave of pairs: adjacent block pairs share every
   // K/V tile (256 query rows per staged tile; +6.5 % at C3 over the single-block kernel).
-  // MFA_FWD_SHARE=0 keeps the single-block kernel (A/B).
+  // MFA_FWD_SHARE=0 keeps the single-block kernel (A/B), =1 takes the shared-tile kernel at
+  // any size (tests).
   const char* sv = getenv("MFA_FWD_SHARE");
-  const bool adj = !(sv && sv[0] == '0') && !p.mask.causal && !p.mask.window && !var &&
-                   (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256;
+  const bool adj = !p.mask.causal && !p.mask.window && !var &&
+                   (sv ? sv[0] == '1' : (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);
 #define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                          \
   if (elem == ELEM && DP == DPV && adj)                                         \
     return launch_fwd2_share<EE, DPV, BKV, false>(p, stream);                   \
@@ -911,8 +916,10 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   MFA_F2(P_BF16, BF16, 64, 64, 2)
   MFA_F2(P_BF16, BF16, 128, 64, 2)
 #undef MFA_F2
-  if (elem == P_FP16 && DP == 256) return launch_fwd2<F16, 256, 32, 2>(p, stream);
-  if (elem == P_BF16 && DP == 256) return launch_fwd2<BF16, 256, 32, 2>(p, stream);
+  if (elem == P_FP16 && DP == 256)
+    return adj ? launch_fwd2_share<F16, 256, 32, false>(p, stream) : launch_fwd2<F16, 256, 32, 2>(p, stream);
+  if (elem == P_BF16 && DP == 256)
+    return adj ? launch_fwd2_share<BF16, 256, 32, false>(p, stream) : launch_fwd2<BF16, 256, 32, 2>(p, stream);
   return hipErrorNotSupported;
 }
 
@@ -929,6 +936,8 @@ MFA_F2_INST(BF16, 128, 64, 2)
 #undef MFA_F2_INST
 template __global__ void mfa_fwd2_pair_kernel<F16, 128, 64, 4, false>(FwdParams);
 template __global__ void mfa_fwd2_kernel<F16, 256, 32, 2>(FwdParams);
+template __global__ void mfa_fwd2_share_kernel<F16, 256, 32, false>(FwdParams);
+template __global__ void mfa_fwd2_share_kernel<BF16, 256, 32, false>(FwdParams);
 template __global__ void mfa_fwd2_kernel<BF16, 256, 32, 2>(FwdParams);
 
 }  // namespace mfa

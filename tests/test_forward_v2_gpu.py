@@ -179,3 +179,20 @@ def test_v2_pair_kernel_forced(gpu, mask, R, C, pair):
     finally:
         os.environ.pop("MFA_FWD_VARIANT", None)
         os.environ.pop("MFA_FWD_PAIR", None)
+
+
+@pytest.mark.parametrize("prec", [FP16, BF16])
+@pytest.mark.parametrize("R,C,D", [(256, 256, 64), (384, 300, 128), (200, 333, 128),
+                                   (130, 130, 256), (520, 96, 256), (129, 64, 72)])
+def test_v2_adjacent_share_forced(gpu, R, C, D, prec):
+    # The shared-tile kernel on adjacent block pairs (picked by default for unmasked forwards
+    # with >= 256 pairs, e.g. C3 and C5's forward), forced at small sizes: odd block counts
+    # (group 1 without rows), R and C off the tile grid, D below the padded width.
+    B, H = 1, 2
+    Q = gaussian((B, H, R, D), R + D)
+    K, V = gaussian((B, H, C, D), C), gaussian((B, H, C, D), C + 1)
+    os.environ["MFA_FWD_SHARE"] = "1"
+    try:
+        check(Q, K, V, prec)
+    finally:
+        os.environ.pop("MFA_FWD_SHARE", None)

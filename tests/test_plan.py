@@ -48,7 +48,7 @@ def test_small_unmasked_runs_single_block_kernel():
 def test_c5_forward_and_backward_phases():
     d = mh(8, 32, 4096, 256)
     f = one(mfa.multihead_plan(d))
-    assert f["name"].startswith("mfa_fwd2_kernel<F16, 256, 32, 2")
+    assert f["name"] == "mfa_fwd2_share_kernel<F16, 256, 32, false>"
     q = one(mfa.multihead_plan(d, K.backwardQuery))
     kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
     assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32>"
@@ -86,7 +86,7 @@ def test_misaligned_query_falls_back_to_generic_kernel():
 def test_quantized_plans():
     base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
     qi = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, integer_matmul=True)
-    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 128, 2>"
+    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 128, 2, 2>"
     # Dequant-exact: one dequantisation pass per quantised operand (kv_dequant.hip), then the
     # tuned 16-bit kernel on the dense copies.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)

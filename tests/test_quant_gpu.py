@@ -3,6 +3,8 @@ arithmetic), quantized forward/backward (QuantizedAttentionTest gates: INT8 relE
 FP16 < 0.05, blockwise INT8 < 0.15; QuantizedAttentionTest.swift:441-791) and the
 dequant-exact property: with per-tensor scales the kernel's result equals attention on the
 dequantised K/V up to fp32 rounding."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -401,6 +403,28 @@ def test_integer_matmul_forward(gpu, B, H, Hkv, R, C, D, causal, window, qp):
     assert relerr(o, ref["O"]) < I8MM_REL
     assert maxerr(l, ref["L"]) < I8MM_L
     assert relerr(o, ol.attention(Q, K, V, causal=causal, window=window)["O"]) < 0.25
+
+
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,qp", [
+    (2, 4, 4, 200, 200, 128, P.FP16),   # odd block count: group 1 of the last pair has no rows
+    (1, 4, 2, 257, 129, 96, P.BF16),
+    (1, 3, 1, 384, 1000, 128, P.FP16),
+])
+def test_integer_matmul_shared_tiles_forced(gpu, B, H, Hkv, R, C, D, qp):
+    # Two 4-wave groups on adjacent blocks sharing every staged tile (the default for unmasked
+    # C3-sized problems), forced at small sizes; same gates as above.
+    rng = np.random.default_rng(R * 5 + C)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
+    os.environ["MFA_I8_SHARE"] = "1"
+    try:
+        o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8, integer_matmul=True)
+    finally:
+        os.environ.pop("MFA_I8_SHARE", None)
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"])
+    assert np.isfinite(o.cpu().numpy()).all()
+    assert relerr(o, ref["O"]) < I8MM_REL
+    assert maxerr(l, ref["L"]) < I8MM_L
 
 
 def test_integer_matmul_ineligible_falls_back_exact(gpu):

@@ -30,6 +30,9 @@ def main():
     if a.cfg == "C2D64":
         B, H, S, D = 1, 32, 4096, 64
         causal = True
+    if a.cfg == "C5F":  # C5's forward on a 2-batch slice
+        B, H, S, D = 2, 32, 4096, 256
+        causal = False
     q, k, v = (((torch.rand((B, H, S, D), generator=g, device=dev) * 2 - 1) * 0.25).half()
                for _ in range(3))
     i8 = a.cfg == "C3I8"
