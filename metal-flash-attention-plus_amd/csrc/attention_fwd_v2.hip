@@ -868,10 +868,6 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   const char* var = getenv("MFA_FWD_VARIANT");
-  if (!var) {
-    const hipError_t e3 = fwd3_dispatch(p, elem, DP, stream);
-    if (e3 != hipErrorNotSupported) return e3;
-  }
   const int blocks = p.nblk * p.B * p.H;
   bool single = !p.mask.causal || blocks > 768 || DP > 128;
   if (var && var[0] == 's') single = true;

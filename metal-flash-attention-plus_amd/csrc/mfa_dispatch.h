@@ -61,7 +61,6 @@ hipError_t kv_dequant_dispatch(const Operand& op, int B, int Hx, int S, int D, i
                                void* out, hipStream_t stream);
 // Third-generation 16-bit forward at D = 128, no mask or causal (attention_fwd_v3.hip);
 // hipErrorNotSupported otherwise.
-hipError_t fwd3_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 hipError_t fwd_fast_dispatch(const FwdParams& p, int elem, int DP, int kvsrc, hipStream_t stream);
 // INT8 K/V on the integer matrix cores (attention_fwd_i8.hip); 128-query blocks.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream);

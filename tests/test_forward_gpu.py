@@ -7,6 +7,8 @@ Cases follow the reference's own tests (paths relative to the reference repo):
     strided BSHD == contiguous bit-exact, BF16 inputs 5e-3 (KernelRegressionTests.swift:238-512);
   - BASELINE.json config 1 (1 head fp32 S128 D64) and config 2 at full size on one head.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -115,6 +117,38 @@ def test_strided_bshd_matches_contiguous_bitexact(gpu, prec):
                                            value_strides=strides)
     torch.cuda.synchronize()
     assert torch.equal(o, o_ref)
+
+
+@pytest.mark.parametrize("causal,share", [(False, "1"), (True, None)])
+def test_strided_bshd_gqa_shared_tile_kernels(gpu, causal, share):
+    # The shared-tile kernels (adjacent unmasked pairs, forced at this size; mirrored causal
+    # pairs, the default) with BSHD strides, GQA (4 query heads per kv head) and B = 2: equal
+    # to the contiguous BHSD run bit for bit, and to the oracle.
+    B, H, Hkv, S, D = 2, 8, 2, 640, 128
+    rng = np.random.default_rng(640)
+    Qn = rng.standard_normal((B, H, S, D)).astype(np.float32)
+    Kn = rng.standard_normal((B, Hkv, S, D)).astype(np.float32)
+    Vn = rng.standard_normal((B, Hkv, S, D)).astype(np.float32)
+    if share:
+        os.environ["MFA_FWD_SHARE"] = share
+    try:
+        o_ref, _ = run_forward(Qn, Kn, Vn, prec=FP16, causal=causal)
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=FP16, causal=causal)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D, Hkv=Hkv)
+        to_bshd = lambda x: to_device(np.ascontiguousarray(x.transpose(0, 2, 1, 3)), FP16)
+        qs = [S * H * D, D, H * D, 1]
+        ks = [S * Hkv * D, D, Hkv * D, 1]
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device="cuda:0")
+        mfa.MultiHeadAttention().encodeForward(desc, to_bshd(Qn), to_bshd(Kn), to_bshd(Vn), o,
+                                               query_strides=qs, key_strides=ks, value_strides=ks)
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("MFA_FWD_SHARE", None)
+    assert torch.equal(o, o_ref)
+    for b, hh in ((0, 0), (1, 5)):
+        ref = ol.attention(seen(Qn[b:b + 1, hh:hh + 1], FP16), seen(Kn[b:b + 1, hh // 4:hh // 4 + 1], FP16),
+                           seen(Vn[b:b + 1, hh // 4:hh // 4 + 1], FP16), causal=causal)
+        assert np.abs(o[b, hh].cpu().numpy() - ref["O"][0, 0]).max() <= 5e-3
 
 
 def test_forward_without_logsumexp_matches(gpu):

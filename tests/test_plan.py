@@ -112,8 +112,8 @@ def test_quantized_plans():
 
 def test_environment_override_is_visible_in_plan(monkeypatch):
     d = mh(1, 16, 4096, 128, causal=True)
-    monkeypatch.setenv("MFA_FWD3", "1")
-    assert one(mfa.multihead_plan(d))["name"].startswith("fwd3::mfa_fwd3_kernel<F16, true")
+    monkeypatch.setenv("MFA_FWD_PAIR", "o")
+    assert one(mfa.multihead_plan(d))["name"] == "mfa_fwd2_pair_kernel<F16, 128, 64, 4, true>"
     monkeypatch.setenv("MFA_DISABLE_FAST", "1")
     assert one(mfa.multihead_plan(d))["name"].startswith("mfa_fwd_kernel<")
 

@@ -4,7 +4,6 @@
 // Prints, per stamp slot, the spread over waves of (slot time − kernel's first start), µs.
 #define MFA_STAMPS 1
 #include "../../metal-flash-attention-plus_amd/csrc/attention_fwd_v2.hip"
-#include "../../metal-flash-attention-plus_amd/csrc/attention_fwd_v3.hip"  // fwd3_dispatch
 
 #include <algorithm>
 #include <cstring>

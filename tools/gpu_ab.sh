@@ -2,7 +2,7 @@
 # GPU box: full -m gpu suite, then interleaved A/B of forward variants (development).
 # Usage: bash tools/gpu_ab.sh TAG "KNOB=a,b" "cfg1 cfg2 ..."
 set -o pipefail
-TAG=${1:-ab}; KNOB=${2:-MFA_FWD3=1,0}; CFGS=${3:-"C2 C3"}
+TAG=${1:-ab}; KNOB=${2:-MFA_FWD_SHARE=0,1}; CFGS=${3:-"C2 C3"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
