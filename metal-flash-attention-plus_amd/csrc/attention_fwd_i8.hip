@@ -332,7 +332,8 @@ hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) 
   // (MFA_I8_SHARE=0 keeps one 4-wave workgroup per block, =1 shares at any size: tests).
   const char* sh = getenv("MFA_I8_SHARE");
   if (!small && !p.mask.causal && !p.mask.window &&
-      (sh ? sh[0] == '1' : (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256)) {
+      (sh ? sh[0] == '1'
+          : (p.nblk % 2 == 0 || p.nblk >= 8) && (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256)) {
     if (elem == P_FP16) return launch_i8<F16, 128, 2, 2>(p, stream);
     if (elem == P_BF16) return launch_i8<BF16, 128, 2, 2>(p, stream);
   }

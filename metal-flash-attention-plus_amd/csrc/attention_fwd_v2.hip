@@ -897,8 +897,11 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   // MFA_FWD_SHARE=0 keeps the single-block kernel (A/B), =1 takes the shared-tile kernel at
   // any size (tests).
   const char* sv = getenv("MFA_FWD_SHARE");
+  // (An odd block count leaves group 1 of the last pair without rows: not for nblk < 8 odd.)
   const bool adj = !p.mask.causal && !p.mask.window && !var &&
-                   (sv ? sv[0] == '1' : (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);
+                   (sv ? sv[0] == '1'
+                       : (p.nblk % 2 == 0 || p.nblk >= 8) &&
+                             (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);
 #define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                          \
   if (elem == ELEM && DP == DPV && adj)                                         \
     return launch_fwd2_share<EE, DPV, BKV, false>(p, stream);                   \

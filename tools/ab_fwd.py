@@ -30,10 +30,14 @@ def main():
     if a.cfg == "C2D64":
         B, H, S, D = 1, 32, 4096, 64
         causal = True
+    if a.cfg in ("C4A", "C4AF"):  # C4's attention (bf16), and the same shape in fp16
+        B, H, S, D = 1, 16, 4096, 128
+        causal = False
     if a.cfg == "C5F":  # C5's forward on a 2-batch slice
         B, H, S, D = 2, 32, 4096, 256
         causal = False
-    q, k, v = (((torch.rand((B, H, S, D), generator=g, device=dev) * 2 - 1) * 0.25).half()
+    dt = torch.bfloat16 if a.cfg == "C4A" else torch.float16
+    q, k, v = (((torch.rand((B, H, S, D), generator=g, device=dev) * 2 - 1) * 0.25).to(dt)
                for _ in range(3))
     i8 = a.cfg == "C3I8"
     if i8:
@@ -49,7 +53,9 @@ def main():
         tv = mfa.quantized_tensor(vq, mfa.Precision.INT8, scale=vs.item())
     o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
     l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
-    base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16, causal=causal)
+    base = mfa.AttentionDescriptor.make(
+        low_precision=True, precision=mfa.Precision.BF16 if a.cfg == "C4A" else mfa.Precision.FP16,
+        causal=causal)
     desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
     mha = mfa.MultiHeadAttention()
     if i8:
