@@ -30,6 +30,15 @@ def main():
     if a.cfg == "C2D64":
         B, H, S, D = 1, 32, 4096, 64
         causal = True
+    if a.cfg == "C2B4":  # C2 with 4x the batch (2048 causal blocks)
+        B, H, S, D = 4, 16, 4096, 128
+        causal = True
+    if a.cfg == "C2S8":  # causal S8192 (1024 blocks)
+        B, H, S, D = 1, 16, 8192, 128
+        causal = True
+    if a.cfg.startswith("x"):  # xB,H,S,D,causal (0/1)
+        B, H, S, D, cz = (int(t) for t in a.cfg[1:].split(","))
+        causal = bool(cz)
     if a.cfg in ("C4A", "C4AF"):  # C4's attention (bf16), and the same shape in fp16
         B, H, S, D = 1, 16, 4096, 128
         causal = False
