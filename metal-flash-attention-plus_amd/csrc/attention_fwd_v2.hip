@@ -869,7 +869,10 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   const char* var = getenv("MFA_FWD_VARIANT");
   const int blocks = p.nblk * p.B * p.H;
-  bool single = !p.mask.causal || blocks > 768 || DP > 128;
+  // Causal: mirrored pairs while they fill at most ~1.5 rounds of the chip, or up to 3 rounds
+  // for long rows (S >= 8192: 64 blocks; one-process A/B: H16 S8192 1057 vs 987 TF single,
+  // B2 H16 S8192 1027 vs 1043, B2 H16 S4096 881 vs 889).
+  bool single = !p.mask.causal || DP > 128 || (blocks > 768 && !(p.nblk >= 64 && blocks <= 1536));
   if (var && var[0] == 's') single = true;
   if (var && var[0] == 'p') single = false;
   // Development A/B of the scheduling knobs on the fp16 D=128 single-block kernel.
