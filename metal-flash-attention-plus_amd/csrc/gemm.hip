@@ -165,7 +165,10 @@ __global__ void __launch_bounds__(256) mfa_gemm_kernel(GemmParams p) {
 //   * A [128 m][64 k] and B [64 k][128 n] tiles land by LDS-DMA in the TileA image, double
 //     buffered, one barrier per 64-deep k-step; B^T fragments by transposed reads, A fragments
 //     in the matching k order as two 8-byte reads.
-template <class E>
+// LAY: 0 = NN; 1 = NT (B stored [N][K]: its tile is a [128 n][64 k] image like A's, both
+// operands read by rows in the natural k order); 2 = TN (A stored [K][M]: its tile is a
+// [64 k][128 m] image like B's, both operands read transposed in the permuted k order).
+template <class E, int LAY = 0>
 __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
   constexpr int BM = 128, BN = 128, BK = 64;
   using TAa = TileA<BK>;   // A tile: 128 rows of 64 k (128 B)
@@ -193,12 +196,18 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) abase[c] = TAa::off(wm * 64 + l32, c) + 8 * hh;
 
-  DmaA<BK, BM, 256> ad;   // 128-byte rows
-  DmaA<BN, BK, 256> bd;   // 256-byte rows
-  ad.init(p.lda * 2, BM, BK * 2, tid);
-  bd.init(p.ldb * 2, BK, BN * 2, tid);
-  const char* ahead = A + (int64_t)m0 * p.lda * 2;
-  const char* bhead = B + (int64_t)n0 * 2;
+  // Tile images: A [128 m][64 k] (NN, NT) or [64 k][128 m] (TN); B [64 k][128 n] (NN, TN) or
+  // [128 n][64 k] (NT).  Same byte size either way.
+  constexpr bool AK = LAY != 2, BKR = LAY == 1;  // A / B rows are k-contiguous
+  DmaA<AK ? BK : BM, AK ? BM : BK, 256> ad;
+  DmaA<BKR ? BK : BN, BKR ? BN : BK, 256> bd;
+  ad.init(p.lda * 2, AK ? BM : BK, (AK ? BK : BM) * 2, tid);
+  bd.init(p.ldb * 2, BKR ? BN : BK, (BKR ? BK : BN) * 2, tid);
+  const char* ahead = A + (AK ? (int64_t)m0 * p.lda * 2 : (int64_t)m0 * 2);
+  const char* bhead = B + (BKR ? (int64_t)n0 * p.ldb * 2 : (int64_t)n0 * 2);
+  const int64_t astep = AK ? 2 : (int64_t)p.lda * 2;   // bytes per k
+  const int64_t bstep = BKR ? 2 : (int64_t)p.ldb * 2;
+  const int rb[2] = {TAa::row_base(l32, hh, 0), TAa::row_base(l32, hh, 1)};
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -213,28 +222,42 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
   int cur = 0;
   for (int k0 = 0; k0 < p.K; k0 += BK) {
     if (k0 + BK < p.K) {
-      ad.issue(ahead + (int64_t)(k0 + BK) * 2, 0, ab + (cur ^ 1) * ATILE);
-      bd.issue(bhead + (int64_t)(k0 + BK) * p.ldb * 2, 0, bb + (cur ^ 1) * BTILE);
+      ad.issue(ahead + (int64_t)(k0 + BK) * astep, 0, ab + (cur ^ 1) * ATILE);
+      bd.issue(bhead + (int64_t)(k0 + BK) * bstep, 0, bb + (cur ^ 1) * BTILE);
     }
     const char* at = ab + cur * ATILE;
     const char* bt = bb + cur * BTILE;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       i16x8 af[2], bf[2];
+      if constexpr (LAY == 1) {
+        // Both k-contiguous images: rows read in the natural k order (chunk 2s + hh).
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        // rows wm*64 + 32i + l32: + 32 rows = 4 row blocks of TAa::RB; chunks 2s, 2s+1 live
-        // in column block s/2 (512 B) at chunk parities (2s)&3, (2s+1)&3.
-        const int cb = 512 * ((2 * s) >> 2);
-        const uint2 lo = *reinterpret_cast<const uint2*>(at + abase[(2 * s) & 3] + cb +
-                                                         TAa::RB * 4 * i);
-        const uint2 hi = *reinterpret_cast<const uint2*>(at + abase[(2 * s + 1) & 3] + cb +
-                                                         TAa::RB * 4 * i);
-        af[i] = __builtin_bit_cast(i16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        for (int i = 0; i < 2; ++i)
+          af[i] = *reinterpret_cast<const i16x8*>(TAa::row_addr(at, rb, 2 * wm + i, s));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bf[j] = *reinterpret_cast<const i16x8*>(TAa::row_addr(bt, rb, 2 * wn + j, s));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if constexpr (LAY == 2) {
+            af[i] = AB::read_tr_a(at, trb, 32 * (s >> 1), s & 1, wm * 64 + i * 32);
+          } else {
+            // rows wm*64 + 32i + l32: + 32 rows = 4 row blocks of TAa::RB; chunks 2s, 2s+1
+            // live in column block s/2 (512 B) at chunk parities (2s)&3, (2s+1)&3.
+            const int cb = 512 * ((2 * s) >> 2);
+            const uint2 lo = *reinterpret_cast<const uint2*>(at + abase[(2 * s) & 3] + cb +
+                                                             TAa::RB * 4 * i);
+            const uint2 hi = *reinterpret_cast<const uint2*>(at + abase[(2 * s + 1) & 3] + cb +
+                                                             TAa::RB * 4 * i);
+            af[i] = __builtin_bit_cast(i16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bf[j] = AB::read_tr_a(bt, trb, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bf[j] = AB::read_tr_a(bt, trb, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -260,8 +283,12 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + ci) =
               make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
         } else {
-          const uint32_t w0 = (uint32_t)E::from_f32(a[4 * g]) | ((uint32_t)E::from_f32(a[4 * g + 1]) << 16);
-          const uint32_t w1 = (uint32_t)E::from_f32(a[4 * g + 2]) | ((uint32_t)E::from_f32(a[4 * g + 3]) << 16);
+          // C's own 16-bit format (it may differ from the operands').
+          auto cv = [&](float x) -> uint32_t {
+            return p.prec_c == P_FP16 ? (uint32_t)f32_to_f16(x) : (uint32_t)f32_to_bf16(x);
+          };
+          const uint32_t w0 = cv(a[4 * g]) | (cv(a[4 * g + 1]) << 16);
+          const uint32_t w1 = cv(a[4 * g + 2]) | (cv(a[4 * g + 3]) << 16);
           *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + ci) = make_uint2(w0, w1);
         }
       }
@@ -271,9 +298,10 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
 template <class E>
 static hipError_t launch_gemm2(const GemmParams& p, int batch, hipStream_t stream) {
   constexpr int LDS = 2 * (128 * 64 * 2) + 2 * (64 * 128 * 2);
-  auto kern = mfa_gemm2_kernel<E>;
   const dim3 grid(p.N / 128, p.M / 128, batch);
-  return launch(kern, grid, dim3(256), LDS, stream, p);
+  if (p.trans_b) return launch(mfa_gemm2_kernel<E, 1>, grid, dim3(256), LDS, stream, p);
+  if (p.trans_a) return launch(mfa_gemm2_kernel<E, 2>, grid, dim3(256), LDS, stream, p);
+  return launch(mfa_gemm2_kernel<E, 0>, grid, dim3(256), LDS, stream, p);
 }
 
 static bool gemm2_eligible(const GemmParams& p) {
@@ -286,13 +314,21 @@ static bool gemm2_eligible(const GemmParams& p) {
   if (!al(p.a) || !al(p.b[0]) || !al(p.c[0])) return false;
   if (p.b[1] && (!al(p.b[1]) || !al(p.c[1]))) return false;
   if (!p.b[1] && (p.sa % 8 || p.sb % 8 || p.sc % 8)) return false;
+  if (p.trans_a && p.trans_b) return false;  // TT: the general kernel
   // 32-bit buffer offsets per tile stream.
-  if ((int64_t)p.M * p.lda * 2 >= ((int64_t)1 << 31) || (int64_t)p.K * p.ldb * 2 >= ((int64_t)1 << 31))
+  const int64_t arows = p.trans_a ? p.K : p.M, brows = p.trans_b ? p.N : p.K;
+  if (arows * p.lda * 2 >= ((int64_t)1 << 31) || brows * p.ldb * 2 >= ((int64_t)1 << 31))
     return false;
   return true;
 }
 
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream) {
+  if (p.trans_a || p.trans_b) {  // NT / TN: whole tiles on gemm2, else the caller's fallback
+    if (!gemm2_eligible(p)) return hipErrorNotSupported;
+    if (prec_ab == P_FP16) return launch_gemm2<F16>(p, batch, stream);
+    if (prec_ab == P_BF16) return launch_gemm2<BF16>(p, batch, stream);
+    return hipErrorNotSupported;
+  }
   if (gemm2_eligible(p)) {
     if (prec_ab == P_FP16) return launch_gemm2<F16>(p, batch, stream);
     if (prec_ab == P_BF16) return launch_gemm2<BF16>(p, batch, stream);
@@ -307,8 +343,12 @@ hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_
   return hipGetLastError();
 }
 
-template __global__ void mfa_gemm2_kernel<F16>(GemmParams);
-template __global__ void mfa_gemm2_kernel<BF16>(GemmParams);
+template __global__ void mfa_gemm2_kernel<F16, 0>(GemmParams);
+template __global__ void mfa_gemm2_kernel<BF16, 0>(GemmParams);
+template __global__ void mfa_gemm2_kernel<F16, 1>(GemmParams);
+template __global__ void mfa_gemm2_kernel<BF16, 1>(GemmParams);
+template __global__ void mfa_gemm2_kernel<F16, 2>(GemmParams);
+template __global__ void mfa_gemm2_kernel<BF16, 2>(GemmParams);
 
 }  // namespace mfa
 
@@ -381,7 +421,17 @@ extern "C" mfa_status_t mfa_gemm_kernel_descriptor(const mfa_gemm_descriptor_t* 
   out->grid_y = (d->M + 127) / 128;
   out->grid_z = d->batch ? d->batch : 1;
   const char* cn = pl.compute == mfa::P_FP16 ? "f16" : pl.compute == mfa::P_BF16 ? "bf16" : "f32";
-  if (pl.tuned) {
+  const bool tile_t = !pl.tuned && pl.compute != mfa::P_FP32 &&
+                      (d->transpose_a != d->transpose_b) && !d->load_previous_c &&
+                      d->M % 128 == 0 && d->N % 128 == 0 && d->K % 64 == 0 && d->K > 0 &&
+                      pl.lda % 8 == 0 && pl.ldb % 8 == 0 && pl.ldc % 8 == 0;
+  if (tile_t) {
+    // Whole tiles, one transpose: the LDS-DMA kernel (16-byte aligned buffers; the general
+    // kernel otherwise).
+    out->threadgroup_memory_allocation = 2 * (128 * 64 * 2 + 64 * 128 * 2);
+    snprintf(out->variant, sizeof(out->variant), "mfa_gemm2_kernel<%s,%s>/mfa_gemm_general_kernel",
+             cn, d->transpose_a ? "TN" : "NT");
+  } else if (pl.tuned) {
     out->threadgroup_memory_allocation = 2 * (128 * 32 * 2 + 32 * 128 * 2);
     snprintf(out->variant, sizeof(out->variant), "mfa_gemm_kernel<%s>/mfa_gemm2_kernel<%s>", cn, cn);
   } else {
@@ -401,7 +451,28 @@ extern "C" mfa_status_t mfa_gemm(const mfa_gemm_descriptor_t* d, const void* A, 
   if (st != MFA_SUCCESS) return st;
   if (d->M == 0 || d->N == 0) return MFA_SUCCESS;
   const int batch = d->batch ? (int)d->batch : 1;
-  hipError_t e;
+  hipError_t e = hipErrorNotSupported;
+  // NT / TN with equal 16-bit operands and whole 128x128x64 tiles: the LDS-DMA kernel.
+  if (!pl.tuned && pl.compute != P_FP32 && (d->transpose_a != d->transpose_b) &&
+      !d->load_previous_c) {
+    GemmParams p{};
+    p.a = A;
+    p.b[0] = B;
+    p.b[1] = nullptr;
+    p.c[0] = C;
+    p.M = (int)d->M; p.N = (int)d->N; p.K = (int)d->K;
+    p.lda = (int)pl.lda; p.ldb = (int)pl.ldb; p.ldc = (int)pl.ldc;
+    p.sa = (int64_t)d->stride_a; p.sb = (int64_t)d->stride_b; p.sc = (int64_t)d->stride_c;
+    p.prec_c = d->precision_c;
+    p.trans_a = d->transpose_a ? 1 : 0;
+    p.trans_b = d->transpose_b ? 1 : 0;
+    e = gemm_dispatch(p, d->precision_a, batch, (hipStream_t)stream);
+    if (e == hipSuccess) return MFA_SUCCESS;
+    if (e != hipErrorNotSupported) {
+      mfa_api_set_error("mfa_gemm: kernel launch failed");
+      return MFA_ERR_LAUNCH;
+    }
+  }
   if (pl.tuned) {
     GemmParams p{};
     p.a = A;

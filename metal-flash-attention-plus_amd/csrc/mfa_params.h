@@ -73,6 +73,7 @@ struct GemmParams {
   int64_t sa, sb, sc;     // batch strides (elements) when b[1] == nullptr
   int32_t prec_c;         // P_FP32 / P_FP16 / P_BF16
   int32_t load_prev;
+  int32_t trans_a, trans_b;  // A stored [K][M] / B stored [N][K] (mfa_gemm2_kernel TN / NT)
 };
 
 // MLA latent-space attention (attention_mla_latent.hip): query rows of every head of a batch

@@ -163,6 +163,40 @@ def test_batched_transposed(gpu, prec, ta, tb):
     assert np.max(np.abs(c.cpu().numpy() - ref)) < tol
 
 
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False)])
+@pytest.mark.parametrize("prec,pc", [(P.FP16, P.FP32), (P.BF16, P.BF16), (P.BF16, P.FP16)])
+def test_whole_tile_transposed_lds_dma(gpu, prec, pc, ta, tb):
+    # NT / TN with equal 16-bit operands and whole 128x128x64 tiles run mfa_gemm2_kernel (both
+    # operands read by rows, or both transposed); C in its own precision; batched, with padded
+    # leading dimensions (NaN padding catches any read outside the logical matrices).
+    Bn, M, N, K, pad = 2, 256, 384, 192, 8
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((Bn, M, K)).astype(np.float32)
+    Bm = rng.standard_normal((Bn, K, N)).astype(np.float32)
+    a_log = A.transpose(0, 2, 1) if ta else A
+    b_log = Bm.transpose(0, 2, 1) if tb else Bm
+    lda, ldb = a_log.shape[2] + pad, b_log.shape[2] + pad
+    a_full = np.full((Bn, a_log.shape[1], lda), np.nan, dtype=np.float32)
+    a_full[:, :, :a_log.shape[2]] = a_log
+    b_full = np.full((Bn, b_log.shape[1], ldb), np.nan, dtype=np.float32)
+    b_full[:, :, :b_log.shape[2]] = b_log
+    a = torch.from_numpy(a_full).to(DEV).to(TORCH_DTYPE[prec])
+    b = torch.from_numpy(b_full).to(DEV).to(TORCH_DTYPE[prec])
+    c = torch.full((Bn, M, N), float("nan"), dtype=torch.float32, device=DEV).to(TORCH_DTYPE[pc])
+    mfa.gemm(a, b, c, M, N, K, prec, pc, transpose_a=ta, transpose_b=tb, batch=Bn,
+             lda=lda, ldb=ldb, stride_a=a_full[0].size, stride_b=b_full[0].size, stride_c=M * N)
+    torch.cuda.synchronize()
+    As, Bs = seen(A, prec), seen(Bm, prec)
+    ref = seen(np.stack([ol.gemm(As[i], Bs[i]) for i in range(Bn)]).astype(np.float32), pc)
+    got = c.float().cpu().numpy()
+    assert np.isfinite(got).all()
+    tol = 1e-3 * np.sqrt(K) + (0 if pc == P.FP32 else 8e-3 * np.abs(ref).max())
+    assert np.max(np.abs(got - ref)) < tol
+    d = mfa.gemm_descriptor(M, N, K, prec, pc, transpose_a=ta, transpose_b=tb, batch=Bn,
+                            lda=lda, ldb=ldb)
+    assert b"mfa_gemm2_kernel" in mfa.gemm_kernel_descriptor(d).variant
+
+
 def test_zero_k_and_empty(gpu):
     # K = 0: C = 0 (or C itself with loadPreviousC); M = 0 / N = 0: nothing written.
     c = torch.full((5, 6), float("nan"), dtype=torch.float32, device=DEV)
