@@ -165,9 +165,11 @@ __global__ void __launch_bounds__(256) mfa_gemm_kernel(GemmParams p) {
 //   * A [128 m][64 k] and B [64 k][128 n] tiles land by LDS-DMA in the TileA image, double
 //     buffered, one barrier per 64-deep k-step; B^T fragments by transposed reads, A fragments
 //     in the matching k order as two 8-byte reads.
-// LAY: 0 = NN; 1 = NT (B stored [N][K]: its tile is a [128 n][64 k] image like A's, both
-// operands read by rows in the natural k order); 2 = TN (A stored [K][M]: its tile is a
-// [64 k][128 m] image like B's, both operands read transposed in the permuted k order).
+// LAY: 3 = NN (A by rows, B by transposed reads in the natural k order, TileA::tr_base_nat);
+// 0 = NN with the permuted order of TileA::tr_base (A read as two 8-byte halves to match);
+// 1 = NT (B stored [N][K]: its tile is a [128 n][64 k] image like A's, both operands read by
+// rows); 2 = TN (A stored [K][M]: its tile is a [64 k][128 m] image like B's, both operands
+// read transposed in the permuted k order).
 template <class E, int LAY = 0>
 __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
   constexpr int BM = 128, BN = 128, BK = 64;
@@ -198,7 +200,7 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
 
   // Tile images: A [128 m][64 k] (NN, NT) or [64 k][128 m] (TN); B [64 k][128 n] (NN, TN) or
   // [128 n][64 k] (NT).  Same byte size either way.
-  constexpr bool AK = LAY != 2, BKR = LAY == 1;  // A / B rows are k-contiguous
+  constexpr bool AK = LAY != 2, BKR = LAY == 1;  // A / B rows are k-contiguous (LAY 3 = NN)
   DmaA<AK ? BK : BM, AK ? BM : BK, 256> ad;
   DmaA<BKR ? BK : BN, BKR ? BN : BK, 256> bd;
   ad.init(p.lda * 2, AK ? BM : BK, (AK ? BK : BM) * 2, tid);
@@ -208,6 +210,7 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
   const int64_t astep = AK ? 2 : (int64_t)p.lda * 2;   // bytes per k
   const int64_t bstep = BKR ? 2 : (int64_t)p.ldb * 2;
   const int rb[2] = {TAa::row_base(l32, hh, 0), TAa::row_base(l32, hh, 1)};
+  const int trn[2] = {TBb::tr_base_nat(lane, 0), TBb::tr_base_nat(lane, 1)};
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -230,7 +233,15 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       i16x8 af[2], bf[2];
-      if constexpr (LAY == 1) {
+      if constexpr (LAY == 3) {
+        // NN, natural k order: A by 16-byte row reads, B by transposed reads whose lane halves
+        // take rows 8h..8h+7 of the k-step (TileA::tr_base_nat).
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          af[i] = *reinterpret_cast<const i16x8*>(TAa::row_addr(at, rb, 2 * wm + i, s));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = AB::read_tr_nat(bt, trn, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
+      } else if constexpr (LAY == 1) {
         // Both k-contiguous images: rows read in the natural k order (chunk 2s + hh).
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -301,7 +312,11 @@ static hipError_t launch_gemm2(const GemmParams& p, int batch, hipStream_t strea
   const dim3 grid(p.N / 128, p.M / 128, batch);
   if (p.trans_b) return launch(mfa_gemm2_kernel<E, 1>, grid, dim3(256), LDS, stream, p);
   if (p.trans_a) return launch(mfa_gemm2_kernel<E, 2>, grid, dim3(256), LDS, stream, p);
-  return launch(mfa_gemm2_kernel<E, 0>, grid, dim3(256), LDS, stream, p);
+  // NN in the natural k order (4096^3 fp16: 856-959 vs 745-749 TF for the permuted order;
+  // C4 151.3 vs 153.1 us).  MFA_GEMM_NN=0 keeps the permuted-order kernel (A/B).
+  const char* nn = getenv("MFA_GEMM_NN");
+  if (nn && nn[0] == '0') return launch(mfa_gemm2_kernel<E, 0>, grid, dim3(256), LDS, stream, p);
+  return launch(mfa_gemm2_kernel<E, 3>, grid, dim3(256), LDS, stream, p);
 }
 
 static bool gemm2_eligible(const GemmParams& p) {
@@ -349,6 +364,8 @@ template __global__ void mfa_gemm2_kernel<F16, 1>(GemmParams);
 template __global__ void mfa_gemm2_kernel<BF16, 1>(GemmParams);
 template __global__ void mfa_gemm2_kernel<F16, 2>(GemmParams);
 template __global__ void mfa_gemm2_kernel<BF16, 2>(GemmParams);
+template __global__ void mfa_gemm2_kernel<F16, 3>(GemmParams);
+template __global__ void mfa_gemm2_kernel<BF16, 3>(GemmParams);
 
 }  // namespace mfa
 

@@ -139,6 +139,14 @@ struct TileA {
     return 64 * (4 * h + (i >> 2)) + 16 * ((2 * g + ((i >> 1) & 1)) ^ (h ^ (2 * half))) +
            8 * (i & 1);
   }
+  // Natural-order variant: lane half h receives rows 8h..8h+3 (half 0) and 8h+4..8h+7 (half 1)
+  // of a 16-row k-step, i.e. k = 8h + j in register order, as a row read of a k-contiguous
+  // image gives.  Each 32-lane half still reads 256 contiguous bytes (conflict-free).
+  __device__ static __forceinline__ int tr_base_nat(int lane, int half) {
+    const int h = (lane >> 5) & 1, g = (lane >> 4) & 1, i = lane & 15;
+    return RB * h + 64 * (4 * half + (i >> 2)) +
+           16 * ((2 * g + ((i >> 1) & 1)) ^ (2 * h + half)) + 8 * (i & 1);
+  }
 };
 
 // Arithmetic policy for 16-bit operands (f16 or bf16 MFMA, K = 16 per instruction).
@@ -192,6 +200,21 @@ struct Arith16 {
         (__attribute__((address_space(3))) i16x4_tr*)(tile + trb[0] + o));
     i16x4_tr hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (__attribute__((address_space(3))) i16x4_tr*)(tile + trb[1] + o + RB));
+    frag f;
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+    f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+    return f;
+  }
+  // read_tr_a with tr_base_nat bases: k-step s of the 32-key sub-tile at row kb, natural k
+  // order (k = 16s + 8h + j).
+  __device__ static __forceinline__ frag read_tr_nat(const char* tile, const int (&trn)[2], int kb,
+                                                    int s, int dcol) {
+    constexpr int RB = TileA<DP>::RB;
+    const int o = RB * (kb / 8 + 2 * s) + 512 * (dcol / 32);
+    i16x4_tr lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) i16x4_tr*)(tile + trn[0] + o));
+    i16x4_tr hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) i16x4_tr*)(tile + trn[1] + o));
     frag f;
     f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
     f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Interleaved one-process A/B of an environment knob on the C4 MLA forward (decompression
-GEMMs + attention), with a bit-identity check against the first arm (development tool).
+GEMMs + attention), checked against the first arm at bf16 tolerance (development tool).
 Usage: python tools/ab_mla.py VAR=a,b [--rounds N]"""
 import argparse
 import json
@@ -46,8 +46,9 @@ def main():
             if ref is None:
                 ref = (o.clone(), kb.clone(), vb.clone())
             else:
-                assert torch.equal(kb, ref[1]) and torch.equal(vb, ref[2]), f"{var}={x}: K/V differ"
-                assert torch.equal(o, ref[0]), f"{var}={x}: O differs"
+                for got, want in ((kb, ref[1]), (vb, ref[2]), (o, ref[0])):
+                    assert torch.allclose(got.float(), want.float(), rtol=1e-2, atol=1e-3), \
+                        f"{var}={x}: result differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):

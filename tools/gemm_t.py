@@ -6,7 +6,9 @@ n = 4096
 a = (torch.rand((n, n), device='cuda') - 0.5).half()
 b = (torch.rand((n, n), device='cuda') - 0.5).half()
 c = torch.empty((n, n), device='cuda', dtype=torch.float16)
-for ta, tb in ((0, 0), (0, 1), (1, 0), (1, 1)):
+import os
+for ta, tb, nn in ((0, 0, '0'), (0, 0, '3'), (0, 1, '0'), (1, 0, '0'), (0, 0, '0'), (0, 0, '3')):
+    os.environ['MFA_GEMM_NN'] = nn
     f = lambda: mfa.gemm(a, b, c, n, n, n, P.FP16, P.FP16, transpose_a=bool(ta), transpose_b=bool(tb))
     for _ in range(5): f()
     torch.cuda.synchronize()
@@ -17,4 +19,4 @@ for ta, tb in ((0, 0), (0, 1), (1, 0), (1, 1)):
     ms = e0.elapsed_time(e1) / 20
     ref = (a.float().T if ta else a.float()) @ (b.float().T if tb else b.float())
     err = (c.float() - ref).abs().max().item()
-    print(f"T{ta}{tb} {ms:.4f} ms {2*n**3/ms/1e9:.1f} TF maxerr {err:.3e}")
+    print(f"T{ta}{tb} nn{nn} {ms:.4f} ms {2*n**3/ms/1e9:.1f} TF maxerr {err:.3e}")
