@@ -155,10 +155,11 @@ def test_v2_config2_shape_rows(gpu, prec):
         assert (l[0, hh].double() - ref_l).abs().max().item() <= 7e-3
 
 
+@pytest.mark.parametrize("D", [128, 64])
 @pytest.mark.parametrize("pair", ["share", "o"])
 @pytest.mark.parametrize("mask", [None, "causal", ("window", 50)])
 @pytest.mark.parametrize("R,C", [(200, 200), (129, 1000), (340, 300), (1000, 129)])
-def test_v2_pair_kernel_forced(gpu, mask, R, C, pair):
+def test_v2_pair_kernel_forced(gpu, mask, R, C, pair, D):
     # The mirrored-pair kernels on shapes they are not picked for by default: odd block counts,
     # non-causal, windows, R != C (R > C: both blocks of a pair end at the last key, so the
     # shared-tile schedule has no second phase).  "share": the shared-tile schedule (default for
@@ -166,7 +167,7 @@ def test_v2_pair_kernel_forced(gpu, mask, R, C, pair):
     # groups merged through LDS per block).
     if isinstance(mask, tuple) and R > C + mask[1]:
         pytest.skip("rows past C + window are masked everywhere (not a v2 case)")
-    B, H, D = 1, 2, 128
+    B, H = 1, 2
     Q = gaussian((B, H, R, D), R)
     K, V = gaussian((B, H, C, D), C), gaussian((B, H, C, D), C + 1)
     kw = {"causal": True} if mask == "causal" else ({"window": mask[1]} if mask else {})
