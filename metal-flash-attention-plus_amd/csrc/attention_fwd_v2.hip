@@ -286,7 +286,20 @@ __device__ __forceinline__ void store_l(const FwdParams& p, float L, int b, int 
     reinterpret_cast<float*>(p.l)[li] = L;
 }
 
-template <int DP>
+// 16 bytes of O; NT: a non-temporal (streaming) store.  Only for whole-row stores (the O row
+// image): O is written once, and the final drain of every CU at once is the mirrored kernel's
+// tail (C2 +2.4-2.8 %).  Row-per-lane stores (16-32 B per row and instruction) lose with NT
+// (C3 -4.9 %, C5 forward -11.5 %): their partial lines are no longer merged in L2.
+template <bool NT>
+__device__ __forceinline__ void st_o4(float* dst, float a, float b, float c, float d) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  if constexpr (NT)
+    __builtin_nontemporal_store(f4v{a, b, c, d}, reinterpret_cast<f4v*>(dst));
+  else
+    *reinterpret_cast<f4v*>(dst) = f4v{a, b, c, d};
+}
+
+template <int DP, bool NT = false>
 __device__ __forceinline__ void store_o_l(const FwdParams& p, const f32x16 (&o)[DP / 32],
                                           float m, float l, int b, int h, int qi, int hh) {
   const float inv = p.o_mul / l;
@@ -297,9 +310,8 @@ __device__ __forceinline__ void store_o_l(const FwdParams& p, const f32x16 (&o)[
     for (int g = 0; g < 4; ++g) {
       const int d = dt * 32 + 8 * g + 4 * hh;
       if (d < p.D)
-        *reinterpret_cast<float4*>(orow + d) =
-            make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
-                        o[dt][4 * g + 3] * inv);
+        st_o4<NT>(orow + d, o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
+                  o[dt][4 * g + 3] * inv);
     }
   if (hh == 0) {
     const float L = m + __log2f(l);
@@ -626,7 +638,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // ring 1 (group 1's), group 0's Q staging: 160 KiB at D = 128.
 // MIRROR = false (no mask): the pair is two adjacent blocks (2·pi, 2·pi + 1) with the same key
 // range, so every step is a shared one (256 query rows per K/V tile).
-template <class E, int DP, int BK, bool MIRROR>
+template <class E, int DP, int BK, bool MIRROR, bool NTS = false>
 __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   constexpr int NT = 256, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
@@ -818,9 +830,11 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   for (int k = 0; k < OST; ++k) {
     const int idx = k * 2 * NT + tid;
     const int r = idx / CPR, d = (idx % CPR) * 4;
-    if (q0 + r < p.R && d < p.D)
-      *reinterpret_cast<float4*>(obase + (int64_t)(q0 + r) * p.o_ss + d) =
-          *reinterpret_cast<const float4*>(mbase + r * ORS + d * 4);
+    if (q0 + r < p.R && d < p.D) {
+      const float4 v = *reinterpret_cast<const float4*>(mbase + r * ORS + d * 4);
+      float4* dst = reinterpret_cast<float4*>(obase + (int64_t)(q0 + r) * p.o_ss + d);
+      st_o4<NTS>(reinterpret_cast<float*>(dst), v.x, v.y, v.z, v.w);
+    }
   }
 }
 
@@ -836,6 +850,12 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   FwdParams q = p;
   q.nblk = (p.R + 127) / 128;
   const int npairs = (q.nblk + 1) / 2;
+  // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
+  // (A/B).
+  const char* nt = getenv("MFA_SHARE_NT");
+  if (MIRROR && !(nt && nt[0] == '0'))
+    return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true>, dim3(npairs * p.B * p.H),
+                  dim3(512), LDS, stream, q);
   return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR>, dim3(npairs * p.B * p.H), dim3(512),
                 LDS, stream, q);
 }
@@ -930,6 +950,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   template __global__ void mfa_fwd2_pair_kernel<EE, DPV, BKV, 4, true>(FwdParams);  \
   template __global__ void mfa_fwd2_pair_kernel<EE, DPV, 32, 2, true>(FwdParams);  \
   template __global__ void mfa_fwd2_share_kernel<EE, DPV, BKV, true>(FwdParams);  \
+  template __global__ void mfa_fwd2_share_kernel<EE, DPV, BKV, true, true>(FwdParams);  \
   template __global__ void mfa_fwd2_share_kernel<EE, DPV, BKV, false>(FwdParams);
 MFA_F2_INST(F16, 64, 64, 2)
 MFA_F2_INST(F16, 128, 64, 2)
