@@ -638,7 +638,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // ring 1 (group 1's), group 0's Q staging: 160 KiB at D = 128.
 // MIRROR = false (no mask): the pair is two adjacent blocks (2·pi, 2·pi + 1) with the same key
 // range, so every step is a shared one (256 query rows per K/V tile).
-template <class E, int DP, int BK, bool MIRROR, bool NTS = false>
+template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false>
 __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   constexpr int NT = 256, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
@@ -779,6 +779,37 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     // Group 0 holds all of A (if any), group 1 all of B: no merge.
     float l = cross_half_sum(st.lh) + kFltMin;
     if (!(l > 0.f)) l = kFltMin;
+    if constexpr (!MIRROR && IMG) {
+      // Adjacent pairs: both blocks leave through O row images (one per group, over the free
+      // ring) as whole rows from all 8 waves.
+      constexpr int ORS = DP * 4 + 16;
+      const float inv = p.o_mul / l;
+      char* orow = smem + (g * 128 + wg * 32 + l32) * ORS;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          *reinterpret_cast<float4*>(orow + (dt * 32 + 8 * gq + 4 * hh) * 4) =
+              make_float4(st.o[dt][4 * gq] * inv, st.o[dt][4 * gq + 1] * inv,
+                          st.o[dt][4 * gq + 2] * inv, st.o[dt][4 * gq + 3] * inv);
+      if (hh == 0 && qi < p.R) store_l(p, st.m + __log2f(l), b, h, qi);
+      __syncthreads();
+      float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        const int qb = (blk ? rbB : rbA) * BQ;
+#pragma unroll
+        for (int k = 0; k < OST; ++k) {
+          const int idx = k * 2 * NT + tid;
+          const int r = idx / CPR, d = (idx % CPR) * 4;
+          if (qb + r < p.R && d < p.D) {
+            const float4 v = *reinterpret_cast<const float4*>(smem + (blk * 128 + r) * ORS + d * 4);
+            st_o4<NTS>(obase + (int64_t)(qb + r) * p.o_ss + d, v.x, v.y, v.z, v.w);
+          }
+        }
+      }
+      return;
+    }
     if (qi < p.R && (g == 1 || nA > 0)) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
     return;
   }
@@ -846,6 +877,7 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   constexpr int OIMG = 128 * (DP * 4 + 16);
   constexpr int LDS = !MIRROR ? RING
                       : RING > MERGE ? (RING > OIMG ? RING : OIMG) : (MERGE > OIMG ? MERGE : OIMG);
+  constexpr int LDS_IMG = 2 * OIMG > RING ? 2 * OIMG : RING;  // adjacent pairs, two O images
   static_assert(LDS <= 160 * 1024, "LDS");
   FwdParams q = p;
   q.nblk = (p.R + 127) / 128;
@@ -853,6 +885,15 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
   // (A/B).
   const char* nt = getenv("MFA_SHARE_NT");
+  if constexpr (!MIRROR && LDS_IMG <= 160 * 1024) {
+    // Adjacent pairs (D <= 128): both blocks leave through O row images by non-temporal
+    // whole-row stores (C3 +0.8 %, C4's attention +1.9 % in one-process A/B; plain stores
+    // from the images: +0.5 / +0.9 %).  MFA_SHARE_IMG=0 keeps row-per-lane stores (A/B).
+    const char* im = getenv("MFA_SHARE_IMG");
+    if (!(im && im[0] == '0'))
+      return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true>,
+                    dim3(npairs * p.B * p.H), dim3(512), LDS_IMG, stream, q);
+  }
   if (MIRROR && !(nt && nt[0] == '0'))
     return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true>, dim3(npairs * p.B * p.H),
                   dim3(512), LDS, stream, q);
