@@ -289,6 +289,45 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
 
   float l = xh_sum(lh);
   if (!(l > 0.f)) l = kFltMin;
+  if constexpr (NG == 2) {
+    // Both blocks' O leave through LDS row images (one per group, over the free K/V ring and
+    // above it) as whole rows from all 8 waves, by non-temporal stores (as the fp16
+    // shared-tile kernel; O is written once).
+    constexpr int ORS = DP * 4 + 16, CPR = DP / 4, OST = BQ * CPR / NT;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const float inv = p.o_mul / l;
+    char* orow = smem + (grp * BQ + wave * 32 + l32) * ORS;
+#pragma unroll
+    for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f4v*>(orow + (dt * 32 + 8 * g + 4 * hh) * 4) =
+            f4v{(float)oi[dt][4 * g] * inv, (float)oi[dt][4 * g + 1] * inv,
+                (float)oi[dt][4 * g + 2] * inv, (float)oi[dt][4 * g + 3] * inv};
+    if (hh == 0 && qvalid) {
+      const float L = m + __log2f(l) - 6.98868468677217f;
+      const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
+      if (p.l_f16)
+        reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+      else
+        reinterpret_cast<float*>(p.l)[li] = L;
+    }
+    __syncthreads();
+    float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+    const int qb0 = NG * (bid / BH) * BQ;
+#pragma unroll
+    for (int blk = 0; blk < NG; ++blk)
+#pragma unroll
+      for (int k = 0; k < OST; ++k) {
+        const int idx = k * NT + tid;
+        const int r = idx / CPR, d = (idx % CPR) * 4;
+        if (qb0 + blk * BQ + r < p.R && d < p.D)
+          __builtin_nontemporal_store(
+              *reinterpret_cast<const f4v*>(smem + (blk * BQ + r) * ORS + d * 4),
+              reinterpret_cast<f4v*>(obase + (int64_t)(qb0 + blk * BQ + r) * p.o_ss + d));
+      }
+    return;
+  }
   if (qvalid) {
     const float inv = p.o_mul / l;
     float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)qi * p.o_ss;
@@ -315,7 +354,10 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
 
 template <class E, int BK, int OCC, int NG = 1>
 static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
-  constexpr int LDS = 4 * BK * 128;  // K and V, double-buffered
+  // K and V double-buffered; two groups: also the O row images of the epilogue.
+  constexpr int RING = 4 * BK * 128, OIMG = NG * 128 * (128 * 4 + 16);
+  constexpr int LDS = NG == 2 && OIMG > RING ? OIMG : RING;
+  static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = mfa_fwd_i8_kernel<E, 128, BK, OCC, NG>;
   const int units = (p.nblk + NG - 1) / NG;
   return launch(kern, dim3(units * p.B * p.H), dim3(256 * NG), LDS, stream, p);
