@@ -22,6 +22,8 @@
 //     −inf give the same P (exactly 0) and the same O and L.
 // Lazy rescaling (threshold 8 in log2 units, cdna_hip_programming.md T13) is kept: the running
 // max and the −m tile change only when a tile's max exceeds m + 8.
+#include <type_traits>
+
 #include "mfa_stage.h"
 #include "mfa_dispatch.h"
 
@@ -638,7 +640,11 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // ring 1 (group 1's), group 0's Q staging: 160 KiB at D = 128.
 // MIRROR = false (no mask): the pair is two adjacent blocks (2·pi, 2·pi + 1) with the same key
 // range, so every step is a shared one (256 query rows per K/V tile).
-template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false>
+// DV (mirrored pairs with nA >= 2): the prologue waits for K0 and Q only — Q arrives by
+// LDS-DMA like the tiles (group 0 into the Q staging, group 1 into ring 1, unused before
+// phase 2) so that every prologue load is counted by hand — and step 0 waits for V0 between
+// its softmax and its PV.
+template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false>
 __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   constexpr int NT = 256, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
@@ -698,31 +704,47 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     return s < S && i < nB;
   };
 
-  if (nA > 0) {
-    ksh.issue(khead, b0, sk);
-    vsh.issue(vhead, b0, sv);
-  } else {
-    int t;
-    if (tile(0, t)) {
-      kd.issue(khead, t, kb0);
-      vd.issue(vhead, t, vb0);
-    }
-  }
   int q0 = (g == 0 && nA > 0 ? rbA : rbB) * BQ;
   int qi = q0 + wg * 32 + l32;
   i16x8 qf[DP / 16];
-  load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
-  DmaA<DP, 32, 64> qd;  // group 0: B's Q rows of this wave, staged for the switch
+  DmaA<DP, 32, 64> qd;  // this wave's 32 Q rows (group 0: B's, staged for the switch)
   qd.init((int)p.q.ss * 2, p.R, p.D * 2, lane);
   const char* qhead = (const char*)p.q.ptr + ((int64_t)b * p.q.sb + (int64_t)h * p.q.sh) * 2;
   RowState<DP> st;
   st.init();
-  wait_vm();
-  prescale_q2<E, DP>(qf, c);
-  __syncthreads();
+  const bool dv = DV && nA >= 2;
+  if (dv) {
+    char* const qdst = g == 0 ? qstg : smem + 4 * TILEB + wg * QW;
+    ksh.issue(khead, b0, sk);
+    qd.issue(qhead, q0 + wg * 32, qdst);
+    vsh.issue(vhead, b0, sv);
+    constexpr int PV0 = DmaA<DP, BK, 2 * NT>::PPW;  // V0 pieces per wave (the youngest)
+    __builtin_amdgcn_s_waitcnt(0x0F70 | PV0);
+    __syncthreads();
+    using A = Arith16<E, DP>;
+#pragma unroll
+    for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(qdst, rbase, 0, ds);
+    prescale_q2<E, DP>(qf, c);
+  } else {
+    if (nA > 0) {
+      ksh.issue(khead, b0, sk);
+      vsh.issue(vhead, b0, sv);
+    } else {
+      int t;
+      if (tile(0, t)) {
+        kd.issue(khead, t, kb0);
+        vd.issue(vhead, t, vb0);
+      }
+    }
+    load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
+    wait_vm();
+    prescale_q2<E, DP>(qf, c);
+    __syncthreads();
+  }
 
   const bool full_sw = rbA * BQ + BQ <= p.R && p.D == DP;  // every switch store is issued
-  auto step = [&](int s, bool sw) {
+  auto step = [&](int s, bool sw, auto first_c) {
+    constexpr bool FIRST = decltype(first_c)::value;  // step 0 of the deferred-V prologue
     // Stage the next step's tile(s) into the slot read two steps ago.
     const int nx = (s + 1) & 1;
     if (s + 1 < nA) {
@@ -756,7 +778,19 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
       const char* kt = (shared ? sk : kb0) + (s & 1) * TILEB;
       const char* vt = (shared ? sv : vb0) + (s & 1) * TILEB;
       const bool mask_tile = (tc + BK > p.C) || (p.mask.causal && tc + BK - 1 > q0);
-      fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh);
+      if constexpr (FIRST) {
+        // V0 is older than the next shared tile's pieces issued above.
+        constexpr int NPN = 2 * DmaA<DP, BK, 2 * NT>::PPW;
+        f32x16 sc[BK / 32];
+        i16x8 pb[BK / 16];
+        fwd2_qk<E, DP, BK>(kt, rbase, qf, st, sc);
+        fwd2_softmax<E, DP, BK>(st, sc, pb, tc, mask_tile, qi, p, c, wsz, hh);
+        __builtin_amdgcn_s_waitcnt(0x0F70 | NPN);
+        __syncthreads();
+        fwd2_pv<E, DP, BK>(vt, trb, pb, st);
+      } else {
+        fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh);
+      }
     }
     if (sw && full_sw)
       __builtin_amdgcn_s_waitcnt(0x0F70 | (NSW & 15) | ((NSW >> 4) << 14));
@@ -766,13 +800,15 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   };
   // Phase 1 up to its last step, which also stages B's Q rows; group 0 switches at step nA.
   int s = 0;
-  for (; s < nA - 1; ++s) step(s, false);
+  using F0 = std::false_type;
+  if (dv) step(s++, false, std::true_type());
+  for (; s < nA - 1; ++s) step(s, false, F0());
   if (nA > 0 && n2 > 0) {
     if (g == 0) qd.issue(qhead, rbB * BQ + wg * 32, qstg);
-    step(s++, false);
-    step(s++, g == 0);
+    step(s++, false, F0());
+    step(s++, g == 0, F0());
   }
-  for (; s < S; ++s) step(s, false);
+  for (; s < S; ++s) step(s, false, F0());
 
   char* const mbase = smem;  // the rings are free: merge area, then the O row image
   if (n2 == 0) {
@@ -884,7 +920,13 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   const int npairs = (q.nblk + 1) / 2;
   // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
   // (A/B).
+  // Mirrored pairs: deferred V0 (+1.2 % at C2 in one-process A/B) and non-temporal O image
+  // stores by default; MFA_SHARE_DV=0 / MFA_SHARE_NT=0 turn them off (A/B).
+  const char* dvv = getenv("MFA_SHARE_DV");
   const char* nt = getenv("MFA_SHARE_NT");
+  if (MIRROR && !(dvv && dvv[0] == '0') && !(nt && nt[0] == '0'))
+    return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, false, true>,
+                  dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
   if constexpr (!MIRROR && LDS_IMG <= 160 * 1024) {
     // Adjacent pairs (D <= 128): both blocks leave through O row images by non-temporal
     // whole-row stores (C3 +0.8 %, C4's attention +1.9 % in one-process A/B; plain stores

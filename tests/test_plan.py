@@ -25,7 +25,7 @@ def one(plan):
 # C5 B8 H32 S4096 D256 fwd + bwd.
 def test_c2_headline_runs_shared_tile_pair_kernel():
     p = one(mfa.multihead_plan(mh(1, 16, 4096, 128, causal=True)))
-    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, true, true, false>"
+    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, true, true, false, true>"
     assert p["threads"] == 512 and p["lds_bytes"] == 160 * 1024  # two rings + Q staging
     # 32 query blocks of 128 rows per head, mirrored in pairs: 16 x 16 heads.
     assert p["workgroups"] == 16 * 16
@@ -34,7 +34,7 @@ def test_c2_headline_runs_shared_tile_pair_kernel():
 def test_c3_runs_adjacent_shared_tile_kernel():
     # Unmasked with >= 256 block pairs: adjacent 128-row blocks share every K/V tile.
     p = one(mfa.multihead_plan(mh(1, 16, 8192, 128)))
-    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true>"
+    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>"
     assert p["threads"] == 512 and p["workgroups"] == 32 * 16
 
 
@@ -48,7 +48,7 @@ def test_small_unmasked_runs_single_block_kernel():
 def test_c5_forward_and_backward_phases():
     d = mh(8, 32, 4096, 256)
     f = one(mfa.multihead_plan(d))
-    assert f["name"] == "mfa_fwd2_share_kernel<F16, 256, 32, false, false, false>"
+    assert f["name"] == "mfa_fwd2_share_kernel<F16, 256, 32, false, false, false, false>"
     q = one(mfa.multihead_plan(d, K.backwardQuery))
     kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
     assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32>"
@@ -62,7 +62,7 @@ def test_bf16_and_d64_instantiations():
     assert one(mfa.multihead_plan(mh(1, 4, 1024, 128, prec=P.BF16)))["name"].startswith(
         "mfa_fwd2_kernel<BF16, 128")
     assert one(mfa.multihead_plan(mh(1, 16, 4096, 64, causal=True)))["name"] == \
-        "mfa_fwd2_share_kernel<F16, 64, 64, true, true, false>"
+        "mfa_fwd2_share_kernel<F16, 64, 64, true, true, false, true>"
 
 
 def test_fp32_inputs_take_generic_kernel():
@@ -92,7 +92,7 @@ def test_quantized_plans():
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(qx)]
     assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
-    assert names[2] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true>" and len(names) == 3
+    assert names[2] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>" and len(names) == 3
     for kind, kern in ((K.backwardQuery, "mfa_bwd_q_fast_kernel<F16, 128, 64>"),
                        (K.backwardKeyValue, "mfa_bwd_kv_fast_kernel<F16, 128, 64>")):
         assert [r["name"] for r in mfa.quantized_plan(qx, kind)][2] == kern
@@ -100,7 +100,7 @@ def test_quantized_plans():
     q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(q4)]
     assert names[:3] == ["mfa_kv_dequant_kernel<F16, 2>"] * 2 + ["mfa_kv_dequant_kernel<F16, 1>"]
-    assert names[3] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true>"
+    assert names[3] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>"
     # A non-zero zero point leaves the integer-matmul kernel (dequant-exact path instead).
     zp = mfa.QuantizedTensor(None, int(P.INT8), 0.5, 3)
     assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_share_kernel<")
