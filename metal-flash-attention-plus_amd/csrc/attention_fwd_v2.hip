@@ -640,6 +640,8 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // ring 1 (group 1's), group 0's Q staging: 160 KiB at D = 128.
 // MIRROR = false (no mask): the pair is two adjacent blocks (2·pi, 2·pi + 1) with the same key
 // range, so every step is a shared one (256 query rows per K/V tile).
+// IMG: adjacent pairs — both blocks' O through LDS row images; mirrored pairs — A's O at the
+// switch through the wave's Q staging region.
 // DV (mirrored pairs with nA >= 2): the prologue waits for K0 and Q only — Q arrives by
 // LDS-DMA like the tiles (group 0 into the Q staging, group 1 into ring 1, unused before
 // phase 2) so that every prologue load is counted by hand — and step 0 waits for V0 between
@@ -762,13 +764,58 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
       // these stores, so the step's counted wait below leaves them in flight).
       float l = cross_half_sum(st.lh) + kFltMin;
       if (!(l > 0.f)) l = kFltMin;
-      if (qi < p.R) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
-      __asm__ __volatile__("" ::: "memory");
-      q0 = rbB * BQ;
-      qi = q0 + wg * 32 + l32;
       using A = Arith16<E, DP>;
+      if constexpr (MIRROR && IMG) {
+        // B's Q rows first (this wave's staging region is then free), then A's O leaves
+        // through that region in two column halves: the wave writes its 32 rows (row per
+        // lane, 16-byte chunks XOR-swizzled by row) and reads them back as whole half-rows,
+        // so each store instruction covers 4 rows x DP*2 contiguous bytes (row-per-lane stores
+        // touched 32 rows x 32 B); wave-private, so no barrier.  Same store count (NSW).
+        char* const wreg = qstg;  // this wave's staging region
 #pragma unroll
-      for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(qstg, rbase, 0, ds);
+        for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(wreg, rbase, 0, ds);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): Q is in registers
+        constexpr int HB = DP * 2, NCH = DP / 8;  // bytes and 16-byte chunks per half-row
+        const float inv = p.o_mul / l;
+        const int qa0 = q0 + wg * 32;
+        float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+          for (int dt = 0; dt < ND / 2; ++dt)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+              const int cch = dt * 8 + 2 * gq + hh;
+              const f32x16& o = st.o[half * (ND / 2) + dt];
+              *reinterpret_cast<float4*>(wreg + l32 * HB + ((cch ^ (l32 & (NCH - 1))) * 16)) =
+                  make_float4(o[4 * gq] * inv, o[4 * gq + 1] * inv, o[4 * gq + 2] * inv,
+                              o[4 * gq + 3] * inv);
+            }
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          constexpr int RPI = 64 / NCH;  // rows per read instruction
+#pragma unroll
+          for (int k = 0; k < 32 / RPI; ++k) {
+            const int r = k * RPI + lane / NCH, j = lane % NCH;
+            const float4 v =
+                *reinterpret_cast<const float4*>(wreg + r * HB + ((j ^ (r & (NCH - 1))) * 16));
+            const int col = half * (DP / 2) + 4 * j;
+            if (qa0 + r < p.R && col < p.D)
+              st_o4<NTS>(obase + (int64_t)(qa0 + r) * p.o_ss + col, v.x, v.y, v.z, v.w);
+          }
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next half's writes
+        }
+        if (hh == 0 && qi < p.R) store_l(p, st.m + __log2f(l), b, h, qi);
+        __asm__ __volatile__("" ::: "memory");
+        q0 = rbB * BQ;
+        qi = q0 + wg * 32 + l32;
+      } else {
+        if (qi < p.R) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+        __asm__ __volatile__("" ::: "memory");
+        q0 = rbB * BQ;
+        qi = q0 + wg * 32 + l32;
+#pragma unroll
+        for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(qstg, rbase, 0, ds);
+      }
       prescale_q2<E, DP>(qf, c);
       st.init();
     }
@@ -924,9 +971,16 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   // stores by default; MFA_SHARE_DV=0 / MFA_SHARE_NT=0 turn them off (A/B).
   const char* dvv = getenv("MFA_SHARE_DV");
   const char* nt = getenv("MFA_SHARE_NT");
-  if (MIRROR && !(dvv && dvv[0] == '0') && !(nt && nt[0] == '0'))
-    return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, false, true>,
+  // ... and A's O at the switch leaves through the wave's Q staging region as whole
+  // half-rows (+0.8 % at C2; MFA_SHARE_SWI=0 keeps row-per-lane stores there).
+  const char* swi = getenv("MFA_SHARE_SWI");
+  if (MIRROR && !(dvv && dvv[0] == '0') && !(nt && nt[0] == '0')) {
+    if (swi && swi[0] == '0')
+      return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, false, true>,
+                    dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
+    return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true, true>,
                   dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
+  }
   if constexpr (!MIRROR && LDS_IMG <= 160 * 1024) {
     // Adjacent pairs (D <= 128): both blocks leave through O row images by non-temporal
     // whole-row stores (C3 +0.8 %, C4's attention +1.9 % in one-process A/B; plain stores

@@ -25,7 +25,7 @@ def one(plan):
 # C5 B8 H32 S4096 D256 fwd + bwd.
 def test_c2_headline_runs_shared_tile_pair_kernel():
     p = one(mfa.multihead_plan(mh(1, 16, 4096, 128, causal=True)))
-    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, true, true, false, true>"
+    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, true, true, true, true>"
     assert p["threads"] == 512 and p["lds_bytes"] == 160 * 1024  # two rings + Q staging
     # 32 query blocks of 128 rows per head, mirrored in pairs: 16 x 16 heads.
     assert p["workgroups"] == 16 * 16
@@ -62,7 +62,7 @@ def test_bf16_and_d64_instantiations():
     assert one(mfa.multihead_plan(mh(1, 4, 1024, 128, prec=P.BF16)))["name"].startswith(
         "mfa_fwd2_kernel<BF16, 128")
     assert one(mfa.multihead_plan(mh(1, 16, 4096, 64, causal=True)))["name"] == \
-        "mfa_fwd2_share_kernel<F16, 64, 64, true, true, false, true>"
+        "mfa_fwd2_share_kernel<F16, 64, 64, true, true, true, true>"
 
 
 def test_fp32_inputs_take_generic_kernel():
