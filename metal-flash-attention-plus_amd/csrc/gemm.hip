@@ -280,6 +280,38 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
   }
 
   // acc[i][j][r] = C[m = m0 + wm*64 + 32i + l32][n = n0 + wn*64 + 32j + acc_row(r, hh)].
+  if (p.c_img) {
+    // 16-bit C: the waves write their quadrants into a [128 m][128 n] image (row pitch 272 B)
+    // in the ring the loop has released, then the workgroup stores whole 256-B rows (16 lanes
+    // per row) instead of one 8-B piece per row per lane.
+    constexpr int CP = BN * 2 + 16;
+    const bool f16c = p.prec_c == P_FP16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x16& a = acc[i][j];
+          auto cv = [&](float x) -> uint32_t {
+            return f16c ? (uint32_t)f32_to_f16(x) : (uint32_t)f32_to_bf16(x);
+          };
+          const uint32_t w0 = cv(a[4 * g]) | (cv(a[4 * g + 1]) << 16);
+          const uint32_t w1 = cv(a[4 * g + 2]) | (cv(a[4 * g + 3]) << 16);
+          const int row = wm * 64 + i * 32 + l32, col = wn * 64 + j * 32 + 8 * g + 4 * hh;
+          *reinterpret_cast<uint2*>(smem + row * CP + col * 2) = make_uint2(w0, w1);
+        }
+    __syncthreads();
+    const int c16 = tid & 15;
+#pragma unroll
+    for (int it = 0; it < BM / 16; ++it) {
+      const int row = it * 16 + (tid >> 4);
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + row * CP + c16 * 16);
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(C) + coff +
+                                (int64_t)(m0 + row) * p.ldc + n0 + c16 * 8) = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + wm * 64 + i * 32 + l32;
@@ -307,9 +339,15 @@ __global__ void __launch_bounds__(256, 2) mfa_gemm2_kernel(GemmParams p) {
 }
 
 template <class E>
-static hipError_t launch_gemm2(const GemmParams& p, int batch, hipStream_t stream) {
+static hipError_t launch_gemm2(const GemmParams& p0, int batch, hipStream_t stream) {
   constexpr int LDS = 2 * (128 * 64 * 2) + 2 * (64 * 128 * 2);
-  const dim3 grid(p.N / 128, p.M / 128, batch);
+  const dim3 grid(p0.N / 128, p0.M / 128, batch);
+  // Whole-row C stores need 16-B aligned rows; MFA_GEMM_IMG=0 keeps the per-lane stores (A/B).
+  GemmParams p = p0;
+  const char* ie = getenv("MFA_GEMM_IMG");
+  auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
+  p.c_img = p.prec_c != P_FP32 && (p.ldc & 7) == 0 && (p.b[1] || (p.sc & 7) == 0) &&
+            al16(p.c[0]) && al16(p.c[1]) && !(ie && ie[0] == '0');
   if (p.trans_b) return launch(mfa_gemm2_kernel<E, 1>, grid, dim3(256), LDS, stream, p);
   if (p.trans_a) return launch(mfa_gemm2_kernel<E, 2>, grid, dim3(256), LDS, stream, p);
   // NN in the natural k order (4096^3 fp16: 856-959 vs 745-749 TF for the permuted order;

@@ -74,6 +74,7 @@ struct GemmParams {
   int32_t prec_c;         // P_FP32 / P_FP16 / P_BF16
   int32_t load_prev;
   int32_t trans_a, trans_b;  // A stored [K][M] / B stored [N][K] (mfa_gemm2_kernel TN / NT)
+  int32_t c_img;          // 16-bit C leaves through an LDS image as whole rows (set by the launcher)
 };
 
 // MLA latent-space attention (attention_mla_latent.hip): query rows of every head of a batch
