@@ -11,6 +11,8 @@ Cases follow the reference's own GEMM tests:
     time, random loadPreviousC; inputs uniform [0, 1) / √K; tolerance createTolerance
     (:317-372) restated below.  Seeded here (the reference draws unseeded).
 The padding of every buffer is NaN, so a read outside the logical matrix shows up."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -209,3 +211,34 @@ def test_zero_k_and_empty(gpu):
     mfa.gemm(a, b, c2, 5, 6, 0, P.FP32, P.FP32, lda=1, ldb=6, load_previous_c=True)
     torch.cuda.synchronize()
     assert torch.all(c2 == 3.0)
+
+
+@pytest.mark.parametrize("img", ["1", "0"])
+@pytest.mark.parametrize("prec,pc", [(P.FP16, P.FP16), (P.BF16, P.BF16), (P.FP16, P.FP32)])
+def test_whole_tile_c_image_padded_ldc(gpu, prec, pc, img):
+    # A 16-bit C leaves mfa_gemm2_kernel through an LDS image as whole rows (default) or as
+    # per-lane pieces (MFA_GEMM_IMG=0); C has a padded leading dimension whose padding, and the
+    # rows past M, must stay untouched (NaN sentinels).
+    Bn, M, N, K, cpad = 2, 256, 256, 128, 8
+    rng = np.random.default_rng(12)
+    A = rng.standard_normal((Bn, M, K)).astype(np.float32)
+    Bm = rng.standard_normal((Bn, K, N)).astype(np.float32)
+    a = torch.from_numpy(A).to(DEV).to(TORCH_DTYPE[prec])
+    b = torch.from_numpy(Bm).to(DEV).to(TORCH_DTYPE[prec])
+    ldc = N + cpad
+    c = torch.full((Bn, M + 1, ldc), float("nan"), dtype=torch.float32, device=DEV).to(TORCH_DTYPE[pc])
+    os.environ["MFA_GEMM_IMG"] = img
+    try:
+        mfa.gemm(a, b, c, M, N, K, prec, pc, batch=Bn, ldc=ldc, stride_a=M * K, stride_b=K * N,
+                 stride_c=(M + 1) * ldc)
+    finally:
+        os.environ.pop("MFA_GEMM_IMG", None)
+    torch.cuda.synchronize()
+    got = c.float().cpu().numpy()
+    assert np.isnan(got[:, :M, N:]).all() and np.isnan(got[:, M]).all()
+    As, Bs = seen(A, prec), seen(Bm, prec)
+    ref = seen(np.stack([ol.gemm(As[i], Bs[i]) for i in range(Bn)]).astype(np.float32), pc)
+    tol = 1e-3 * np.sqrt(K) + (0 if pc == P.FP32 else 8e-3 * np.abs(ref).max())
+    assert np.max(np.abs(got[:, :M, :N] - ref)) < tol
+    d = mfa.gemm_descriptor(M, N, K, prec, pc, batch=Bn, ldc=ldc)
+    assert b"mfa_gemm2_kernel" in mfa.gemm_kernel_descriptor(d).variant
