@@ -42,17 +42,41 @@ def parse():
     ap.add_argument("--no-mla", action="store_true")
     ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8(f) rows")
     ap.add_argument("--c5-batch", type=int, default=8)
+    ap.add_argument("--fake-device", action="store_true",
+                    help="CPU dry run of the launch / rank / timing plumbing (gloo, no GPU, "
+                         "no kernels); used by the CPU test of the --gpus spawn path")
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: run N rank processes under
+    torch.distributed.run (one per GPU, 127.0.0.1 rendezvous) and return their exit code.
+    The parent imports nothing that touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
 
 
 def main():
     args = parse()
-    import torch
-    import mfa_amd as mfa
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.fake_device:
+        return fake_device_run(args, world, rank)
+    import torch
+    import mfa_amd as mfa
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -98,6 +122,19 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / steps
+
+    def timed_steps(fn, n):
+        """n calls of fn bracketed by barrier + synchronize, timed by HIP events on the
+        launch stream; seconds, max over ranks."""
+        barrier()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            fn()
+        e1.record()
+        barrier()
+        return max_over_ranks(e0.elapsed_time(e1) * 1e-3)
 
     import mfa_shard as shard
     H, S, D = args.heads, args.seq, args.dim
@@ -186,12 +223,7 @@ def main():
 
         n5 = 20
         warm(step5)
-        barrier()
-        t5 = time.perf_counter()
-        for _ in range(n5):
-            step5()
-        barrier()
-        el5 = max_over_ranks(time.perf_counter() - t5)
+        el5 = timed_steps(step5, n5)
         f5 = (mfa.attention_flops(B5, H5, S5, S5, D5) +
               mfa.attention_flops(B5, H5, S5, S5, D5, kind="backward"))
         result["fwd_bwd_d256"] = {
@@ -273,13 +305,8 @@ def main():
                             mfa.Precision.BF16, k_buf=kb4, v_buf=vb4, stream=stream)
 
         warm(step4)
-        barrier()
-        t4 = time.perf_counter()
         n4 = 20
-        for _ in range(n4):
-            step4()
-        barrier()
-        el4 = max_over_ranks(time.perf_counter() - t4)
+        el4 = timed_steps(step4, n4)
         f4 = 2 * (2 * B4 * S4 * LAT * H4 * D4) + mfa.attention_flops(B4, H4, S4, S4, D4)
         result["mla"] = {
             "workload": "BASELINE configs[3]: mlaCompressed bf16, latent 512 -> 16 heads x 128 "
@@ -353,6 +380,9 @@ def main():
         step()
     barrier()
     mfa.last_launches()
+    # The timed region: barrier + synchronize on both sides.  The K steps are timed by HIP
+    # events on the launch stream, so `value` carries no host-side launch /
+    # synchronisation latency; the wall clock of the same region is reported beside it.
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -361,7 +391,8 @@ def main():
         step()
     ev1.record()
     barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    wall = max_over_ranks(time.perf_counter() - t0)
+    elapsed = max_over_ranks(ev0.elapsed_time(ev1) * 1e-3)
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel per step on this stream
     flops_step = mfa.attention_flops(B, H, S, S, D, causal=True)
     total_flops = flops_step * args.steps * world
@@ -382,6 +413,11 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "wall_ms_per_step": round(wall / args.steps * 1e3, 4),
+        "wall_value": round(total_flops / wall / 1e12, 2),
+        "timing": "value and ms_per_step: HIP events around the K timed steps on the launch "
+                  "stream, max over ranks; wall_*: host clock of the same barrier-bracketed "
+                  "region (includes launch and synchronisation latency)",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -411,6 +447,35 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def fake_device_run(args, world: int, rank: int):
+    """--fake-device: the rank / barrier / max-over-ranks / JSON plumbing of a real run on
+    the CPU (gloo), with no GPU and no kernels; a step is a no-op.  Lets a CPU test check
+    that `bench.py --gpus N` starts N ranks and reports n_gpus = N."""
+    import torch
+    import torch.distributed as dist_
+    if world > 1:
+        dist_.init_process_group("gloo")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist_.all_reduce(t, op=dist_.ReduceOp.MAX)
+        el = float(t.item())
+        ranks = [None] * world
+        dist_.all_gather_object(ranks, rank)
+    else:
+        ranks = [0]
+    if rank == 0:
+        print(json.dumps({"metric": "fake-device dry run", "value": 0.0, "unit": "none",
+                          "n_gpus": world, "ranks": ranks, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": el / max(args.steps, 1) * 1e3,
+                          "data": "none (--fake-device)"}), flush=True)
+    if world > 1:
+        dist_.destroy_process_group()
 
 
 def pmc_traffic(kernel: str, S: int, H: int, D: int):

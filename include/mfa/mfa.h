@@ -268,8 +268,9 @@ typedef struct mfa_kernel_launch {
 } mfa_kernel_launch_t;
 
 typedef struct mfa_kernel_plan {
-  int32_t count;          /* launches in issue order (0 for empty shapes) */
-  int32_t reserved;
+  int32_t count;          /* launches recorded in `launches`, in issue order (0 for empty shapes) */
+  int32_t total;          /* launches the call issues; total > count means the record holds
+                           * only the first (plan) or last (launch log) four of them */
   mfa_kernel_launch_t launches[4];
 } mfa_kernel_plan_t;
 
@@ -556,6 +557,16 @@ void mfa_sparse_build_block_sparse(const uint8_t* pattern, uint32_t rows, uint32
 const char* mfa_version(void);
 const char* mfa_last_error(void);
 int mfa_abi_version(void);
+
+/* Releases the library scratch (L when the caller passes none, MLA / dequantisation buffers)
+ * held for `stream` on the current device, stream-ordered (hipFreeAsync on that stream);
+ * stream == NULL releases every stream's scratch on the current device.  A caller that
+ * creates short-lived streams calls this before destroying one.  Returns the number of
+ * buffers released.  (No reference counterpart: Metal buffers are reference-counted.) */
+int mfa_release_scratch(void* stream);
+
+/* Diagnostics: (kernel, device) pairs whose dynamic-LDS attribute the library has set. */
+int mfa_kernel_attribute_count(void);
 
 #ifdef __cplusplus
 }

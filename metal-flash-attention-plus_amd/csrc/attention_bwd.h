@@ -54,6 +54,25 @@ __device__ __forceinline__ float mask_value(const BwdParams& p, float s, int q, 
   return m ? kMaskValue : s;
 }
 
+// This lane's half of Σ_d dO[qi, d]·O[qi, d] (computeD, AttentionKernel+Softmax.swift:31-236),
+// from the values in memory (dO registers are FP32 in the reference, Precisions.swift:183-185);
+// lane half hh takes d in [KSTEP/2·hh, KSTEP/2·(hh+1)) of every KSTEP-wide step.
+template <class A>
+__device__ __forceinline__ float rowsum_do_o(const BwdParams& p, int b, int h, int qi, int hh) {
+  const float* orow = p.o + (int64_t)(b * p.H + h) * p.R * p.D + (int64_t)qi * p.o_ss;
+  const int64_t dorow = (int64_t)b * p.dO_op.sb + (int64_t)h * p.dO_op.sh + (int64_t)qi * p.dO_op.ss;
+  float dsum = 0.f;
+  for (int d0 = (A::KSTEP / 2) * hh; d0 < p.D; d0 += A::KSTEP) {
+#pragma unroll
+    for (int j = 0; j < A::KSTEP / 2; ++j) {
+      const int d = d0 + j;
+      if (d < p.D)
+        dsum += load_elem(p.dO_op, dorow + (int64_t)d * p.dO_op.sd) * orow[(int64_t)d * p.o_sd];
+    }
+  }
+  return dsum;
+}
+
 // ---------------------------------------------------------------------------------------
 // backwardQuery: grid = nblk x B x H (1-D, heaviest causal blocks first); NW waves x 32 queries.
 template <class A, int DP, int BT, int NW, int KSRC>
@@ -86,18 +105,7 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_q_kernel(BwdParams p) {
 
   // D = scale · Σ_d dO∘O over the lane's half of the head dimension (computeD), from the
   // values in memory (dO registers are FP32 in the reference, Precisions.swift:183-185).
-  float dsum = 0.f;
-  if (qvalid) {
-    const float* orow = p.o + row * p.D;
-    const int64_t dorow = (int64_t)b * p.dO_op.sb + (int64_t)h * p.dO_op.sh + (int64_t)qi * p.dO_op.ss;
-    for (int d0 = (A::KSTEP / 2) * hh; d0 < p.D; d0 += A::KSTEP) {
-#pragma unroll
-      for (int j = 0; j < A::KSTEP / 2; ++j) {
-        const int d = d0 + j;
-        if (d < p.D) dsum += load_elem(p.dO_op, dorow + (int64_t)d * p.dO_op.sd) * orow[d];
-      }
-    }
-  }
+  float dsum = qvalid ? rowsum_do_o<A>(p, b, h, qi, hh) : 0.f;
   dsum = xhalf_sum(dsum);
   const float Drow = p.dscale * dsum;  // D_sram *= dotProductScale(derivative: true)
   const float Lrow = qvalid ? load_l(p, row) : 0.f;
@@ -204,7 +212,7 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_q_kernel(BwdParams p) {
   }
 
   if (qvalid) {
-    float* out = p.dq + row * p.D;
+    float* out = p.dq + (int64_t)(b * p.H + h) * p.R * p.D + (int64_t)qi * p.dq_ss;
 #pragma unroll
     for (int dt = 0; dt < DP / 32; ++dt) {
 #pragma unroll
@@ -212,7 +220,7 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_q_kernel(BwdParams p) {
         const int d = dt * 32 + 8 * g + 4 * hh;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (d + e < p.D) out[d + e] = dq[dt][4 * g + e] * p.dq_mul;
+          if (d + e < p.D) out[(int64_t)(d + e) * p.dq_sd] = dq[dt][4 * g + e] * p.dq_mul;
       }
     }
   }
@@ -357,9 +365,9 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_kv_kernel(BwdParams p) {
   }
 
   if (kvalid) {
-    const int64_t krow = (int64_t)(b * p.Hkv + kvh) * p.C + ki;
-    float* ok = p.dk + krow * p.D;
-    float* ov = p.dv + krow * p.D;
+    const int64_t slice = (int64_t)(b * p.Hkv + kvh) * p.C * p.D;
+    float* ok = p.dk + slice + (int64_t)ki * p.dk_ss;
+    float* ov = p.dv + slice + (int64_t)ki * p.dv_ss;
 #pragma unroll
     for (int d = 0; d < DP / 32; ++d) {
 #pragma unroll
@@ -368,8 +376,8 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_kv_kernel(BwdParams p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (dd + e < p.D) {
-            ok[dd + e] = dk[d][4 * g + e] * p.dk_mul;
-            ov[dd + e] = dv[d][4 * g + e];
+            ok[(int64_t)(dd + e) * p.dk_sd] = dk[d][4 * g + e] * p.dk_mul;
+            ov[(int64_t)(dd + e) * p.dv_sd] = dv[d][4 * g + e];
           }
       }
     }

@@ -20,33 +20,6 @@
 
 namespace mfa {
 
-template <int NJ>
-__device__ __forceinline__ void apply_masks(f32x16 (&s)[NJ], int kbase, int qi, int hh,
-                                            const FwdParams& p, int b, int h, uint2 range) {
-  const bool qvalid = qi < p.R;
-  const float* arow =
-      (p.mask.amask && qvalid) ? p.mask.amask + ((int64_t)(b * p.H + h) * p.R + qi) * p.C : nullptr;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = kbase + j * 32 + acc_row(i, hh);
-      float x = s[j][i];
-      if (key >= p.C) {
-        x = -__builtin_inff();
-      } else {
-        if (arow) x += arow[key];
-        bool m = false;
-        if (p.mask.causal && key > qi) m = true;
-        if (p.mask.window && (int64_t)qi > (int64_t)key + (int64_t)p.mask.window_size) m = true;
-        if (p.mask.ranges && ((uint32_t)key < range.x || (uint32_t)key >= range.y)) m = true;
-        if (m) x = kMaskValue;
-      }
-      s[j][i] = x;
-    }
-  }
-}
-
 template <class A, int DP, int BK, int NW, int KSRC, int VSRC>
 __global__ void __launch_bounds__(NW * 64) mfa_fwd_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -196,6 +169,7 @@ __global__ void __launch_bounds__(NW * 64) mfa_fwd_kernel(FwdParams p) {
   if (qvalid) {
     const float inv = p.o_mul / l;
     float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)qi * p.o_ss;
+    const bool ovec = p.o_sd == 1 && (p.o_ss & 3) == 0 && (p.D & 3) == 0;
 #pragma unroll
     for (int dt = 0; dt < DP / 32; ++dt) {
 #pragma unroll
@@ -203,7 +177,12 @@ __global__ void __launch_bounds__(NW * 64) mfa_fwd_kernel(FwdParams p) {
         const int d = dt * 32 + 8 * g + 4 * hh;
         const float4 val = make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv,
                                        o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        if (d + 4 <= p.D && (p.D & 3) == 0) {
+        if (p.o_sd != 1) {  // transposed O: element (qi, d) at d * o_sd
+          if (d < p.D) orow[(int64_t)d * p.o_sd] = val.x;
+          if (d + 1 < p.D) orow[(int64_t)(d + 1) * p.o_sd] = val.y;
+          if (d + 2 < p.D) orow[(int64_t)(d + 2) * p.o_sd] = val.z;
+          if (d + 3 < p.D) orow[(int64_t)(d + 3) * p.o_sd] = val.w;
+        } else if (d + 4 <= p.D && ovec) {
           *reinterpret_cast<float4*>(orow + d) = val;
         } else {
           if (d < p.D) orow[d] = val.x;

@@ -53,13 +53,17 @@ int precision_size(int p) {
 
 bool is_quantized(int p) { return p == MFA_PRECISION_INT8 || p == MFA_PRECISION_INT4; }
 
+// Padded head dimension of the register-resident kernels, or 0 above 256: the D-blocked
+// kernels (attention_bigd.hip) take any larger D, as the reference's last parameter-table row
+// does (AttentionDescriptor+Parameters.swift:44-69).
 int pad_head(int D) {
   if (D <= 32) return 32;
   if (D <= 64) return 64;
   if (D <= 128) return 128;
   if (D <= 256) return 256;
-  return -1;
+  return 0;
 }
+constexpr int kBigD = 0;
 
 // Library-owned scratch for buffers the caller does not pass (L in forward:
 // MultiHeadAttention.swift:296-319 allocates one per call; MLA's decompressed K/V, Q~/O~ and
@@ -214,8 +218,6 @@ mfa_status_t plan_masks(const mfa_attention_descriptor_t& base, const void* mask
 // The tuned forward kernel (attention_fwd_fast.hip) covers 16-bit operands with 16-byte aligned
 // rows (8-byte for INT8 K/V), D % 8 == 0, causal / window masks and per-tensor quantisation.
 bool fast_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
-  static const bool disabled = false;
-  (void)disabled;
   if (const char* e = getenv("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return false;
   }
@@ -232,7 +234,7 @@ bool fast_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
   if ((int64_t)p.C * p.k.ss * esz >= ((int64_t)1 << 31) ||
       (int64_t)p.C * p.v.ss * esz >= ((int64_t)1 << 31))
     return false;
-  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1;
+  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1 && p.o_sd == 1;
 }
 
 // attention_fwd_v2.hip: also D = 256, but needs a positive scale and, with causal / window
@@ -253,10 +255,11 @@ bool fwd2_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
   if ((int64_t)p.C * p.k.ss * 2 >= ((int64_t)1 << 31) ||
       (int64_t)p.C * p.v.ss * 2 >= ((int64_t)1 << 31))
     return false;
-  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1;
+  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1 && p.o_sd == 1;
 }
 
 hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, hipStream_t s) {
+  if (DP == kBigD) return mfa::fwd_bigd_dispatch(p, elem, s);
   if (const char* e = getenv("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
   }
@@ -271,19 +274,23 @@ hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, 
   return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
 }
 
-// Transposed layouts the kernels honour: Q, K and V of the multi-head forward (column-major
-// within a head, AttentionKernelDescriptor.swift:34-47).  A transposed O (forward output,
-// backward input and dO) and the transposed gradients the reference writes when Q/K/V are
-// transposed are not implemented: those calls fail instead of writing a dense layout the
-// caller did not ask for.  `qkv_ok` = the call honours transposed Q/K/V.
-mfa_status_t check_transposes(const mfa_attention_descriptor_t& d, bool qkv_ok, const char* what) {
-  if (!d.has_transpose_state) return MFA_SUCCESS;
-  if (d.transpose_o)
-    return fail(MFA_ERR_UNSUPPORTED, "%s: transposed O / dO is not supported", what);
-  if (!qkv_ok && (d.transpose_q || d.transpose_k || d.transpose_v))
-    return fail(MFA_ERR_UNSUPPORTED, "%s: transposed Q/K/V (and gradients) are not supported",
-                what);
+// Transposed layouts (column-major within a head: element (s, d) at d·S + s,
+// AttentionKernelDescriptor.swift:34-47, leadingDimension AttentionKernel.swift:299-313).
+// createTransposeState maps transposeState.O to O and dO and Q / K / V to dQ / dK / dV
+// (AttentionDescriptor.swift:150-165); every entry point honours all of them except the
+// absorbed-MLA extension, whose operands are library-internal (it rejects any).
+mfa_status_t check_transposes(const mfa_attention_descriptor_t& d, bool ok, const char* what) {
+  if (!d.has_transpose_state || ok) return MFA_SUCCESS;
+  if (d.transpose_o || d.transpose_q || d.transpose_k || d.transpose_v)
+    return fail(MFA_ERR_UNSUPPORTED, "%s: transposed operands are not supported", what);
   return MFA_SUCCESS;
+}
+
+// Row / column element strides of an FP32 output (O, dQ, dK, dV) of S rows inside its dense
+// (batch, head) slice of S·D elements.
+void out_strides(int S, int D, bool transposed, int64_t* ss, int64_t* sd) {
+  *ss = transposed ? 1 : D;
+  *sd = transposed ? S : 1;
 }
 
 float resolve_scale(const mfa_attention_descriptor_t& d, int head_dim) {
@@ -306,6 +313,27 @@ const char* mfa_version(void) { return "mfa-cdna4 0.1.0 (gfx950)"; }
 const char* mfa_last_error(void) { return g_last_error.c_str(); }
 
 int mfa_abi_version(void) { return MFA_ABI_VERSION; }
+
+int mfa_release_scratch(void* stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(g_scratch.mu);
+  int n = 0;
+  for (auto it = g_scratch.bufs.begin(); it != g_scratch.bufs.end();) {
+    if (it->first.dev == dev && (!stream || it->first.stream == (hipStream_t)stream)) {
+      if (it->second.first) {
+        (void)hipFreeAsync(it->second.first, it->first.stream);
+        ++n;
+      }
+      it = g_scratch.bufs.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  return n;
+}
+
+int mfa_kernel_attribute_count(void) { return (int)mfa::lds_attr_entries(); }
 
 int mfa_operand_buffer_binding(mfa_operand_t operand) {
   switch (operand) {
@@ -347,27 +375,28 @@ mfa_status_t mfa_attention_kernel_descriptor(const mfa_attention_descriptor_t* d
   if (!desc->has_matrix_dimensions || !desc->has_transpose_state)
     return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
   memset(out, 0, sizeof(*out));
-  {
-    const bool fwd = type == MFA_KERNEL_FORWARD;
-    const mfa_status_t st = check_transposes(*desc, fwd, fwd ? "forward kernel" : "kernel");
-    if (st != MFA_SUCCESS) return st;
-  }
   const Precisions pr = resolve_precisions(*desc);
   const int D = desc->head;
+  if (D <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "head dimension 0");
   const int DP = pad_head(D);
-  if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", D);
   const int elem = elem_of(pr.mem[MFA_OPERAND_Q]);
   if (elem < 0) return fail(MFA_ERR_UNSUPPORTED, "input precision");
   int bp = 0, bt = 0, nw = 0;
-  if (type == MFA_KERNEL_FORWARD || type == MFA_KERNEL_MLA_COMPRESSED)
+  if (DP == kBigD) {
+    bp = 128;
+    bt = 32;
+  } else if (type == MFA_KERNEL_FORWARD || type == MFA_KERNEL_MLA_COMPRESSED) {
     mfa::fwd_block_config(elem, DP, &bp, &bt, &nw);
-  else
+  } else {
     mfa::bwd_block_config(elem, DP, &bp, &bt, &nw);
+  }
   out->block_parallelization = (uint16_t)bp;
   out->block_traversal = (uint16_t)bt;
   // Head block = whole padded head (accumulators stay in registers), clamped to the padded
-  // head dimension as AttentionDescriptor.swift:90-105 does.
-  out->block_head = (uint16_t)std::min(DP, (D + 7) / 8 * 8);
+  // head dimension as AttentionDescriptor.swift:90-105 does; above 256 the head-dimension
+  // chunk the D-blocked kernels stream (the reference's Bd, :96-104 of its README).
+  out->block_head = DP == kBigD ? (uint16_t)(elem == 0 ? mfa::kBigChunk32 : mfa::kBigChunk16)
+                                : (uint16_t)std::min(DP, (D + 7) / 8 * 8);
   out->head_dimension = (uint16_t)D;
   out->sequence_length = std::max(desc->row, desc->column);
   for (int i = 0; i < MFA_OPERAND_COUNT; ++i) {
@@ -411,7 +440,6 @@ mfa_status_t mfa_attention_kernel_create(const mfa_kernel_descriptor_t* k,
     return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
   memset(out, 0, sizeof(*out));
   const int DP = pad_head(k->head_dimension);
-  if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension > 256");
   const int elem = elem_of(k->memory_precisions[MFA_OPERAND_Q]);
   if (elem < 0) return fail(MFA_ERR_UNSUPPORTED, "input precision");
   out->block_parallelization = k->block_parallelization;
@@ -425,17 +453,20 @@ mfa_status_t mfa_attention_kernel_create(const mfa_kernel_descriptor_t* k,
   switch (k->type) {
     case MFA_KERNEL_FORWARD:
     case MFA_KERNEL_MLA_COMPRESSED:
-      out->threadgroup_memory_allocation = (uint32_t)mfa::fwd_lds_bytes(elem, DP);
+      out->threadgroup_memory_allocation =
+          (uint32_t)(DP == kBigD ? mfa::bigd_lds_bytes(0, elem) : mfa::fwd_lds_bytes(elem, DP));
       snprintf(out->variant, sizeof(out->variant), "mfa_fwd_%s_d%d_bq%d_bk%d", en, DP,
                k->block_parallelization, k->block_traversal);
       break;
     case MFA_KERNEL_BACKWARD_QUERY:
-      out->threadgroup_memory_allocation = (uint32_t)mfa::bwd_lds_bytes(0, elem, DP);
+      out->threadgroup_memory_allocation =
+          (uint32_t)(DP == kBigD ? mfa::bigd_lds_bytes(1, elem) : mfa::bwd_lds_bytes(0, elem, DP));
       snprintf(out->variant, sizeof(out->variant), "mfa_bwd_q_%s_d%d_bq%d_bk%d", en, DP,
                k->block_parallelization, k->block_traversal);
       break;
     case MFA_KERNEL_BACKWARD_KEY_VALUE:
-      out->threadgroup_memory_allocation = (uint32_t)mfa::bwd_lds_bytes(1, elem, DP);
+      out->threadgroup_memory_allocation =
+          (uint32_t)(DP == kBigD ? mfa::bigd_lds_bytes(1, elem) : mfa::bwd_lds_bytes(1, elem, DP));
       snprintf(out->variant, sizeof(out->variant), "mfa_bwd_kv_%s_d%d_bk%d_bq%d", en, DP,
                k->block_parallelization, k->block_traversal);
       break;
@@ -543,7 +574,6 @@ mfa_status_t plan_multihead(const mfa_multihead_descriptor_t* desc, const void* 
   if (pl->B <= 0 || pl->H <= 0 || pl->Hkv <= 0 || pl->D <= 0)
     return fail(MFA_ERR_INVALID_DESCRIPTOR, "empty shape");
   pl->DP = pad_head(pl->D);
-  if (pl->DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", pl->D);
   pl->pr = resolve_precisions(base);
   pl->elem = elem_of(pl->pr.mem[MFA_OPERAND_Q]);
   if (pl->elem < 0) return fail(MFA_ERR_UNSUPPORTED, "input precision %d", pl->pr.mem[MFA_OPERAND_Q]);
@@ -561,7 +591,6 @@ extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* 
   MHAPlan pl;
   mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
   if (st != MFA_SUCCESS) return st;
-  if ((st = check_transposes(desc->base, true, "forward")) != MFA_SUCCESS) return st;
   if (pl.R == 0) return MFA_SUCCESS;
   const mfa_attention_descriptor_t& base = desc->base;
   const int prec = pl.pr.mem[MFA_OPERAND_Q];
@@ -572,7 +601,7 @@ extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* 
   p.k = make_operand(buf->K, prec, pl.B, pl.Hkv, pl.C, pl.D, buf->K_strides, base.transpose_k);
   p.v = make_operand(buf->V, prec, pl.B, pl.Hkv, pl.C, pl.D, buf->V_strides, base.transpose_v);
   p.o = (float*)buf->O;
-  p.o_ss = pl.D;
+  out_strides(pl.R, pl.D, base.transpose_o, &p.o_ss, &p.o_sd);
   p.o_sh = (int64_t)pl.R * pl.D;
   p.o_sb = (int64_t)pl.H * pl.R * pl.D;
   p.l_f16 = pl.pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
@@ -604,10 +633,10 @@ int src_kind(int prec) {
 }
 
 mfa_status_t quant_operand(const mfa_quantized_tensor_t* t, int cfg_prec, int B, int Hx, int S,
-                           int D, mfa::Operand* op, float* fold) {
+                           int D, mfa::Operand* op, float* fold, int transposed) {
   if (!t || !t->data) return fail(MFA_ERR_INVALID_ARGUMENT, "null quantized tensor");
   const int prec = cfg_prec;
-  *op = make_operand(t->data, prec, B, Hx, S, D, nullptr, 0);
+  *op = make_operand(t->data, prec, B, Hx, S, D, nullptr, transposed);
   *fold = 1.f;
   if (is_quantized(prec)) {
     if (t->block_scales) {
@@ -635,7 +664,7 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
   if (is_quantized(qp) || kp != MFA_PRECISION_INT8 || vp != MFA_PRECISION_INT8) return false;
   if (p.k.bscale || p.v.bscale || p.k.zp != 0 || p.v.zp != 0) return false;
   if (p.D % 16 != 0 || p.D > 128 || p.mask.amask || p.mask.ranges) return false;
-  if (p.q.sd != 1 || p.k.sd != 1 || p.v.sd != 1) return false;
+  if (p.q.sd != 1 || p.k.sd != 1 || p.v.sd != 1 || p.o_sd != 1) return false;
   if (p.q.ss % 8 || p.q.sh % 8 || p.q.sb % 8) return false;
   if (p.k.ss % 16 || p.k.sh % 16 || p.k.sb % 16) return false;
   if (p.v.ss % 4 || p.v.sh % 4 || p.v.sb % 4) return false;
@@ -649,8 +678,11 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
 // (kv_dequant.hip) when the compute type is 16-bit, D % 8 == 0 and each kv head serves at
 // least 128 query rows: every element is then converted once per call instead of once per
 // query block that reads it, and the tuned 16-bit kernels run (bit-identical operands).
-// Decode-like shapes (few query rows) keep reading the quantised tensors directly.
+// Decode-like shapes (few query rows) keep reading the quantised tensors directly, except
+// above D = 256, where the D-blocked kernels take 16-bit operands only.
+bool dequant_pass_needed(int D) { return pad_head(D) == kBigD; }
 bool dequant_pass_worth(int R, int H, int Hkv, int D, int elem) {
+  if (dequant_pass_needed(D)) return true;
   if (const char* e = getenv("MFA_NO_DEQUANT_PASS")) {
     if (e[0] == '1') return false;
   }
@@ -690,10 +722,12 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   const int H = desc->num_heads ? (int)desc->num_heads : 1;
   const int Hkv = desc->num_kv_heads ? (int)desc->num_kv_heads : H;
   const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
+  if (D <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "head dimension %d", D);
   const int DP = pad_head(D);
-  if (DP < 0 || D <= 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d", D);
-  mfa_status_t st0 = check_transposes(base, false, "quantized forward");
-  if (st0 != MFA_SUCCESS) return st0;
+  const bool tq = base.has_transpose_state && base.transpose_q;
+  const bool tk = base.has_transpose_state && base.transpose_k;
+  const bool tv = base.has_transpose_state && base.transpose_v;
+  const bool to = base.has_transpose_state && base.transpose_o;
   const mfa_quantized_configuration_t& cfg = desc->config;
   const int qp = cfg.query_precision, kp = cfg.key_precision, vp = cfg.value_precision;
   // Compute element type: the floating-point input type, FP16 when every input is integer.
@@ -715,11 +749,12 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   memset(&p, 0, sizeof(p));
   float fq = 1.f, fk = 1.f, fv = 1.f;
   mfa_status_t st;
-  if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq)) != MFA_SUCCESS) return st;
-  if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk)) != MFA_SUCCESS) return st;
-  if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq, tq)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk, tk)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv, tv)) != MFA_SUCCESS) return st;
   p.o = output;
-  p.o_ss = D; p.o_sh = (int64_t)R * D; p.o_sb = (int64_t)H * R * D;
+  out_strides(R, D, to, &p.o_ss, &p.o_sd);
+  p.o_sh = (int64_t)R * D; p.o_sb = (int64_t)H * R * D;
   const Precisions pr = resolve_precisions(base);
   p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
   void* L = logsumexp;
@@ -841,6 +876,8 @@ bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int 
   }
   if (p.mask.amask || p.mask.ranges) return false;
   if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok) return false;
+  // Dense O, dQ, dK, dV rows.
+  if (p.o_sd != 1 || p.dq_sd != 1 || p.dk_sd != 1 || p.dv_sd != 1) return false;
   // Tiles are addressed per head with 32-bit buffer offsets.
   const int64_t lim = (int64_t)1 << 31;
   if ((int64_t)p.C * p.k.ss * 2 >= lim || (int64_t)p.C * p.v.ss * 2 >= lim ||
@@ -854,11 +891,16 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
   mfa::BwdParams p = base_p;
   int bp, bt, nw;
   mfa::bwd_block_config(elem, DP, &bp, &bt, &nw);
-  const bool fast = bwd_fast_eligible(p, elem, DP, ksrc, qsrc);
+  const bool big = DP == kBigD;
+  const bool fast = !big && bwd_fast_eligible(p, elem, DP, ksrc, qsrc);
   if (phase & PHASE_QUERY) {
     p.nblk = (p.R + bp - 1) / bp;
     if (p.R > 0) {
-      hipError_t e = fast ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream) : hipErrorNotSupported;
+      hipError_t e = big    ? mfa::bwd_bigd_dispatch(p, 0, elem, stream)
+                     : fast ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream)
+                            : hipErrorNotSupported;
+      if (big && e == hipErrorNotSupported)
+        return fail(MFA_ERR_UNSUPPORTED, "head dimension %d: mixed operand precisions", p.D);
       if (e == hipErrorNotSupported) e = mfa::bwd_q_dispatch(p, elem, DP, ksrc, ksrc, stream);
       mfa_status_t st = hip_status(e, "mfa_bwd_q launch");
       if (st != MFA_SUCCESS) return st;
@@ -867,7 +909,11 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
   if (phase & PHASE_KV) {
     p.nblk = (p.C + bp - 1) / bp;
     if (p.C > 0) {
-      hipError_t e = fast ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream) : hipErrorNotSupported;
+      hipError_t e = big    ? mfa::bwd_bigd_dispatch(p, 1, elem, stream)
+                     : fast ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream)
+                            : hipErrorNotSupported;
+      if (big && e == hipErrorNotSupported)
+        return fail(MFA_ERR_UNSUPPORTED, "head dimension %d: mixed operand precisions", p.D);
       if (e == hipErrorNotSupported) e = mfa::bwd_kv_dispatch(p, elem, DP, ksrc, qsrc, stream);
       mfa_status_t st = hip_status(e, "mfa_bwd_kv launch");
       if (st != MFA_SUCCESS) return st;
@@ -886,7 +932,6 @@ mfa_status_t multihead_backward(const mfa_multihead_descriptor_t* desc,
   MHAPlan pl;
   mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
   if (st != MFA_SUCCESS) return st;
-  if ((st = check_transposes(desc->base, false, "backward")) != MFA_SUCCESS) return st;
   const mfa_attention_descriptor_t& base = desc->base;
   const int prec = pl.pr.mem[MFA_OPERAND_Q];
   mfa::BwdParams p;
@@ -904,6 +949,10 @@ mfa_status_t multihead_backward(const mfa_multihead_descriptor_t* desc,
   p.dq = (float*)buf->dQ;
   p.dk = (float*)buf->dK;
   p.dv = (float*)buf->dV;
+  out_strides(pl.R, pl.D, base.transpose_o, &p.o_ss, &p.o_sd);
+  out_strides(pl.R, pl.D, base.transpose_q, &p.dq_ss, &p.dq_sd);
+  out_strides(pl.C, pl.D, base.transpose_k, &p.dk_ss, &p.dk_sd);
+  out_strides(pl.C, pl.D, base.transpose_v, &p.dv_ss, &p.dv_sd);
   p.B = pl.B; p.H = pl.H; p.Hkv = pl.Hkv; p.R = pl.R; p.C = pl.C; p.D = pl.D;
   p.group = pl.H / pl.Hkv;
   p.c_log2 = 1.442695041f * pl.scale;
@@ -956,10 +1005,11 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   const int H = desc->num_heads ? (int)desc->num_heads : 1;
   const int Hkv = desc->num_kv_heads ? (int)desc->num_kv_heads : H;
   const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
+  if (D <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "head dimension %d", D);
   const int DP = pad_head(D);
-  if (DP < 0 || D <= 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d", D);
-  mfa_status_t st0 = check_transposes(base, false, "quantized backward");
-  if (st0 != MFA_SUCCESS) return st0;
+  const bool tr = base.has_transpose_state;
+  const bool tq = tr && base.transpose_q, tk = tr && base.transpose_k;
+  const bool tv = tr && base.transpose_v, to = tr && base.transpose_o;
   const mfa_quantized_configuration_t& cfg = desc->config;
   const int qp = cfg.query_precision, kp = cfg.key_precision, vp = cfg.value_precision;
   int elem = -1;
@@ -986,10 +1036,14 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   memset(&p, 0, sizeof(p));
   float fq = 1.f, fk = 1.f, fv = 1.f;
   mfa_status_t st;
-  if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq)) != MFA_SUCCESS) return st;
-  if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk)) != MFA_SUCCESS) return st;
-  if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv)) != MFA_SUCCESS) return st;
-  p.dO_op = make_operand(grad_output, pr.mem[MFA_OPERAND_dO], B, H, R, D, nullptr, 0);
+  if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq, tq)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk, tk)) != MFA_SUCCESS) return st;
+  if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv, tv)) != MFA_SUCCESS) return st;
+  p.dO_op = make_operand(grad_output, pr.mem[MFA_OPERAND_dO], B, H, R, D, nullptr, to);
+  out_strides(R, D, to, &p.o_ss, &p.o_sd);
+  out_strides(R, D, tq, &p.dq_ss, &p.dq_sd);
+  out_strides(C, D, tk, &p.dk_ss, &p.dk_sd);
+  out_strides(C, D, tv, &p.dv_ss, &p.dv_sd);
   p.o = output;
   p.l = logsumexp;
   p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
@@ -1054,6 +1108,7 @@ struct CaptureScope {
   ~CaptureScope() { mfa::plan_capture() = prev; }
   void copy_to(mfa_kernel_plan_t* out) const {
     out->count = cap.count;
+    out->total = cap.total;
     for (int i = 0; i < cap.count; ++i) {
       static_assert(sizeof(out->launches[i].name) == sizeof(cap.rec[i].name), "name size");
       memcpy(out->launches[i].name, cap.rec[i].name, sizeof(out->launches[i].name));
@@ -1102,6 +1157,7 @@ extern "C" int mfa_last_launches(mfa_kernel_plan_t* out) {
   if (out) {
     memset(out, 0, sizeof(*out));
     out->count = (int32_t)n;
+    out->total = (int32_t)std::min<uint64_t>(log.total, 1u << 30);
     for (uint64_t j = 0; j < n; ++j) {
       const int i = (int)((log.total - n + j) % mfa::LaunchLog::kMax);
       mfa::kernel_symbol_name(log.handle[i], out->launches[j].name, sizeof(out->launches[j].name));
@@ -1177,9 +1233,10 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
   const int D = (int)desc->head_dim, Lat = (int)desc->kv_latent_dim;
   if (B <= 0 || H <= 0 || D <= 0 || Lat <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "empty MLA shape");
   const int DP = pad_head(D);
-  if (DP < 0) return fail(MFA_ERR_UNSUPPORTED, "head dimension %d > 256", D);
-  mfa_status_t st0 = check_transposes(desc->base, false, "MLA forward");
-  if (st0 != MFA_SUCCESS) return st0;
+  // The decompressed K/V are written by this call in BSHD (their transpose flags do not
+  // apply); a transposed query and output are honoured.
+  const bool tq = desc->base.has_transpose_state && desc->base.transpose_q;
+  const bool to = desc->base.has_transpose_state && desc->base.transpose_o;
   const int64_t kv_elems = (int64_t)B * Skv * H * D;
   hipStream_t s = (hipStream_t)stream;
   mfa_status_t st;
@@ -1212,11 +1269,12 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
   const int64_t kv_strides[4] = {(int64_t)Skv * H * D, D, (int64_t)H * D, 1};
   mfa::FwdParams p;
   memset(&p, 0, sizeof(p));
-  p.q = make_operand(query, prec, B, H, Sq, D, nullptr, 0);
+  p.q = make_operand(query, prec, B, H, Sq, D, nullptr, tq);
   p.k = make_operand(kb, prec, B, H, Skv, D, kv_strides, 0);
   p.v = make_operand(vb, prec, B, H, Skv, D, kv_strides, 0);
   p.o = output;
-  p.o_ss = D; p.o_sh = (int64_t)Sq * D; p.o_sb = (int64_t)H * Sq * D;
+  out_strides(Sq, D, to, &p.o_ss, &p.o_sd);
+  p.o_sh = (int64_t)Sq * D; p.o_sb = (int64_t)H * Sq * D;
   const Precisions pr = resolve_precisions(desc->base);
   p.l_f16 = pr.mem[MFA_OPERAND_L] == MFA_PRECISION_FP16;
   void* L = logsumexp;

@@ -53,14 +53,24 @@ hipError_t bwd_kv_dispatch(const BwdParams& p, int elem, int DP, int ksrc, int v
 int bwd_lds_bytes(int kind, int elem, int DP);
 // Tuned 16-bit backward phases (attention_bwd_fast.hip); kind 0 = query, 1 = key/value.
 hipError_t bwd_fast_dispatch(const BwdParams& p, int kind, int elem, int DP, hipStream_t stream);
+// D-blocked forward / backward for head dimensions above 256 (attention_bigd.hip): any D,
+// FP32 / FP16 / BF16 operands of one precision (quantised ones arrive dequantised).
+constexpr int kBigChunk16 = 128, kBigChunk32 = 64;  // head-dimension chunk (DC) per element kind
+inline int bigd_lds_bytes(int kind, int elem) {
+  const int dc = elem == 0 ? kBigChunk32 : kBigChunk16;
+  const int row = elem == 0 ? (dc + 1) * 4 : dc * 2;
+  return kind == 0 ? (128 + 2 * 32) * row : 2 * (128 + 32) * row + 2 * 32 * 4;
+}
+hipError_t fwd_bigd_dispatch(const FwdParams& p, int elem, hipStream_t stream);
+hipError_t bwd_bigd_dispatch(const BwdParams& p, int kind, int elem, hipStream_t stream);
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Dense 16-bit copy [B, Hx, S, D] of a quantised operand holding the MFMA operands the
 // dequantise-on-load staging would produce (kv_dequant.hip).
 hipError_t kv_dequant_dispatch(const Operand& op, int B, int Hx, int S, int D, int elem,
                                void* out, hipStream_t stream);
-// Third-generation 16-bit forward at D = 128, no mask or causal (attention_fwd_v3.hip);
-// hipErrorNotSupported otherwise.
+// First-generation tuned 16-bit forward (attention_fwd_fast.hip): D = 64 / 128 16-bit K/V and
+// INT8 K/V at D = 128 dequantised on load; hipErrorNotSupported when the shape is not covered.
 hipError_t fwd_fast_dispatch(const FwdParams& p, int elem, int DP, int kvsrc, hipStream_t stream);
 // INT8 K/V on the integer matrix cores (attention_fwd_i8.hip); 128-query blocks.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream);

@@ -2,8 +2,8 @@
 //
 // Two jobs:
 //   * the dynamic-LDS attribute (hipFuncAttributeMaxDynamicSharedMemorySize) is set once per
-//     device per kernel, under std::call_once, so host threads driving different devices in
-//     one process neither race nor skip a device;
+//     (kernel, device) under a mutex, so host threads driving different devices in one
+//     process neither race nor skip a device or an instantiation;
 //   * plan capture: while a thread has a capture record installed (mfa_multihead_plan,
 //     mfa_attention_kernel_create in mfa_api.cpp), a launch records the kernel instantiation
 //     (its exported symbol, the name rocprofv3 shows), workgroup size, LDS bytes and grid
@@ -19,8 +19,10 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <mutex>
 #include <string>
+#include <utility>
 
 
 namespace mfa {
@@ -35,7 +37,8 @@ struct LaunchRec {
 struct PlanCapture {
   static constexpr int kMax = 4;
   LaunchRec rec[kMax];
-  int count = 0;
+  int count = 0;   // recorded (at most kMax)
+  int total = 0;   // issued
 };
 
 // Installed by the plan API for the duration of one dispatch on this thread (mfa_api.cpp).
@@ -45,19 +48,36 @@ inline PlanCapture*& plan_capture() {
   return cap;
 }
 
-template <class K>
-inline hipError_t set_lds_attr_per_device(K kern, size_t bytes) {
-  static std::once_flag flags[64];
-  static hipError_t errs[64];
+// The attribute state is keyed by (kernel handle, device): every instantiation gets its own
+// hipFuncSetAttribute on every device, whatever its signature.  The value set is the largest
+// LDS size a launch of that kernel has asked for so far on that device.
+struct LdsAttrTable {
+  std::mutex mu;
+  std::map<std::pair<const void*, int>, std::pair<size_t, hipError_t>> set;
+};
+inline LdsAttrTable& lds_attr_table() {
+  static LdsAttrTable t;
+  return t;
+}
+
+inline hipError_t set_lds_attr_per_device(const void* kern, size_t bytes) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  std::call_once(flags[dev], [&] {
-    errs[dev] = hipFuncSetAttribute((const void*)kern,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  });
-  return errs[dev];
+  LdsAttrTable& t = lds_attr_table();
+  std::lock_guard<std::mutex> lock(t.mu);
+  auto it = t.set.find({kern, dev});
+  if (it != t.set.end() && it->second.first >= bytes) return it->second.second;
+  e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  t.set[{kern, dev}] = {bytes, e};
+  return e;
+}
+
+// Number of (kernel, device) pairs whose LDS attribute has been set (tests).
+inline size_t lds_attr_entries() {
+  LdsAttrTable& t = lds_attr_table();
+  std::lock_guard<std::mutex> lock(t.mu);
+  return t.set.size();
 }
 
 // Launch log: the handles and shapes of the launches this thread issued since the log was
@@ -108,6 +128,7 @@ template <class K, class... Args>
 inline hipError_t launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
                          const Args&... args) {
   if (PlanCapture* cap = plan_capture()) {
+    ++cap->total;
     if (cap->count < PlanCapture::kMax) {
       LaunchRec& r = cap->rec[cap->count++];
       kernel_symbol_name((const void*)kern, r.name, sizeof(r.name));
@@ -118,7 +139,7 @@ inline hipError_t launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t 
     return hipSuccess;
   }
   if (lds > 0) {
-    hipError_t e = set_lds_attr_per_device(kern, lds);
+    hipError_t e = set_lds_attr_per_device((const void*)kern, lds);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(kern, grid, block, lds, stream, args...);

@@ -35,7 +35,7 @@ struct MaskArgs {
 struct FwdParams {
   Operand q, k, v;
   float* o;
-  int64_t o_sb, o_sh, o_ss;
+  int64_t o_sb, o_sh, o_ss, o_sd;  // O element strides (o_sd = R: transposeState.O)
   void* l;
   int32_t l_f16;           // L stored as FP16 (lowPrecisionIntermediates)
   int32_t B, H, Hkv, R, C, D;
@@ -52,6 +52,10 @@ struct BwdParams {
   const void* l;  int32_t l_f16;
   void* dD;       int32_t d_bf16;   // D in memory (FP32 or BF16-truncated)
   float* dq;  float* dk;  float* dv;
+  // Row / column element strides inside one (batch, head) slice of O, dQ (slice R·D) and dK,
+  // dV (slice C·D): D and 1 dense, 1 and R (or C) when transposed (AttentionDescriptor.swift:
+  // 150-165 maps transposeState.O to O / dO and Q / K / V to dQ / dK / dV).
+  int64_t o_ss, o_sd, dq_ss, dq_sd, dk_ss, dk_sd, dv_ss, dv_sd;
   int32_t B, H, Hkv, R, C, D;
   int32_t nblk;            // query blocks (bwd_q) or key blocks (bwd_kv) per slice
   int32_t group;           // H / Hkv (query heads per kv head)

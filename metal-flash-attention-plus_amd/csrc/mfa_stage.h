@@ -156,6 +156,13 @@ __device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& 
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Eight 16-bit elements d0..d0+7 of a row at element stride sd (zero past D), packed.
+__device__ __forceinline__ uint4 gather16(const uint16_t* p, int d0, int D, int64_t sd) {
+  auto e = [&](int j) -> uint32_t { return d0 + j < D ? (uint32_t)p[(int64_t)(d0 + j) * sd] : 0u; };
+  return make_uint4(e(0) | (e(1) << 16), e(2) | (e(3) << 16), e(4) | (e(5) << 16),
+                    e(6) | (e(7) << 16));
+}
+
 template <class A, int ROWS, int DP, int NT, int SRC>
 struct Stager {
   static constexpr int CE = 16 / A::ESIZE;   // output elements per 16-byte chunk
@@ -165,8 +172,10 @@ struct Stager {
   uint4 raw[PER];
   uint4 raw2[SRC == SRC_F32ANY ? PER : 1];  // upper 16 bytes of an FP32-stored chunk
 
+  // coff: element offset of the first column (a column chunk [c0, c0 + DP) of a wider
+  // operand: coff = c0 * op.sd, D = columns left from c0); non-quantised sources only.
   __device__ __forceinline__ void load(const Operand& op, int b, int hx, int row0, int nrows,
-                                       int D) {
+                                       int D, int64_t coff = 0) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -176,7 +185,11 @@ struct Stager {
       const int d0 = c * CE;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if ((NCH % NT == 0 || id < NCH) && grow < nrows && d0 < D) {
-        const int64_t rowoff = (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss;
+        const int64_t rowoff =
+            (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss + coff;
+        // Element-wise fallbacks (strided / unaligned rows, the row's last partial chunk)
+        // build the chunk from scalar loads without a local array, so the staging registers
+        // never go through scratch.
         if constexpr (SRC == SRC_F32ANY) {
           if (op.prec == P_FP32) {
             const float* base = (const float*)op.ptr + rowoff;
@@ -184,43 +197,30 @@ struct Stager {
               v = *reinterpret_cast<const uint4*>(base + d0);
               raw2[i] = *reinterpret_cast<const uint4*>(base + d0 + 4);
             } else {
-              uint32_t w[8];
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                w[j] = d0 + j < D ? __builtin_bit_cast(uint32_t, base[(int64_t)(d0 + j) * op.sd]) : 0u;
-              v = make_uint4(w[0], w[1], w[2], w[3]);
-              raw2[i] = make_uint4(w[4], w[5], w[6], w[7]);
+              auto e = [&](int j) -> uint32_t {
+                return d0 + j < D ? __builtin_bit_cast(uint32_t, base[(int64_t)(d0 + j) * op.sd]) : 0u;
+              };
+              v = make_uint4(e(0), e(1), e(2), e(3));
+              raw2[i] = make_uint4(e(4), e(5), e(6), e(7));
             }
           } else {
             const uint16_t* p = (const uint16_t*)op.ptr + rowoff;
             if (op.vec && d0 + 8 <= D) {
               v = *reinterpret_cast<const uint4*>(p + d0);
             } else {
-              uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                if (d0 + j < D) w[j >> 1] |= (uint32_t)p[(int64_t)(d0 + j) * op.sd] << (16 * (j & 1));
-              v = make_uint4(w[0], w[1], w[2], w[3]);
+              v = gather16(p, d0, D, op.sd);
             }
           }
         } else if constexpr (SRC == SRC_SAME) {
           const char* base = (const char*)op.ptr + rowoff * A::ESIZE;
           if (op.vec && d0 + CE <= D) {
             v = *reinterpret_cast<const uint4*>(base + (int64_t)d0 * A::ESIZE);
+          } else if constexpr (A::ESIZE == 2) {
+            v = gather16((const uint16_t*)base, d0, D, op.sd);
           } else {
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            if constexpr (A::ESIZE == 2) {
-              const uint16_t* p = (const uint16_t*)base;
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                if (d0 + j < D) w[j >> 1] |= (uint32_t)p[(int64_t)(d0 + j) * op.sd] << (16 * (j & 1));
-            } else {
-              const uint32_t* p = (const uint32_t*)base;
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                if (d0 + j < D) w[j] = p[(int64_t)(d0 + j) * op.sd];
-            }
-            v = make_uint4(w[0], w[1], w[2], w[3]);
+            const uint32_t* p = (const uint32_t*)base;
+            auto e = [&](int j) -> uint32_t { return d0 + j < D ? p[(int64_t)(d0 + j) * op.sd] : 0u; };
+            v = make_uint4(e(0), e(1), e(2), e(3));
           }
         } else {
           v = load_qchunk<SRC>(op, rowoff, d0, D);
@@ -441,6 +441,36 @@ struct DmaA {
     lds_dma16(head + rb, max(bytes - rb, 0), off[i], dst + n * 1024);
   }
 };
+
+// Forward masks on NJ 32-key accumulators of S^T (key in registers, query qi on the lane):
+// keys past C -> -inf; additive mask; causal / window / sparse-range predicates -> the
+// reference's finite mask value (AttentionKernel+Softmax.swift:243-336).
+template <int NJ>
+__device__ __forceinline__ void apply_masks(f32x16 (&s)[NJ], int kbase, int qi, int hh,
+                                            const FwdParams& p, int b, int h, uint2 range) {
+  const bool qvalid = qi < p.R;
+  const float* arow =
+      (p.mask.amask && qvalid) ? p.mask.amask + ((int64_t)(b * p.H + h) * p.R + qi) * p.C : nullptr;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kbase + j * 32 + acc_row(i, hh);
+      float x = s[j][i];
+      if (key >= p.C) {
+        x = -__builtin_inff();
+      } else {
+        if (arow) x += arow[key];
+        bool m = false;
+        if (p.mask.causal && key > qi) m = true;
+        if (p.mask.window && (int64_t)qi > (int64_t)key + (int64_t)p.mask.window_size) m = true;
+        if (p.mask.ranges && ((uint32_t)key < range.x || (uint32_t)key >= range.y)) m = true;
+        if (m) x = kMaskValue;
+      }
+      s[j][i] = x;
+    }
+  }
+}
 
 // Wait for this wave's outstanding vector-memory operations (LDS-DMA included): vmcnt(0),
 // expcnt / lgkmcnt untouched (gfx9 s_waitcnt encoding).

@@ -204,11 +204,15 @@ class KernelLaunch(ctypes.Structure):
 class KernelPlan(ctypes.Structure):
     _fields_ = [
         ("count", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("total", ctypes.c_int32),
         ("launches", KernelLaunch * 4),
     ]
 
-    def as_list(self) -> list[dict]:
+    def as_list(self, strict: bool = True) -> list[dict]:
+        """The recorded launches; a plan (strict) whose call issues more launches than the
+        record holds raises instead of returning a partial list."""
+        if strict and self.total > self.count:
+            raise MFAError(-1, f"kernel plan truncated: {self.total} launches, {self.count} recorded")
         return [{"name": self.launches[i].name.decode(), "threads": self.launches[i].threads,
                  "lds_bytes": self.launches[i].lds_bytes,
                  "workgroups": self.launches[i].workgroups} for i in range(self.count)]
@@ -376,6 +380,8 @@ _V = ctypes.c_void_p
 _sig("mfa_version", ctypes.c_char_p, [])
 _sig("mfa_last_error", ctypes.c_char_p, [])
 _sig("mfa_abi_version", ctypes.c_int, [])
+_sig("mfa_release_scratch", ctypes.c_int, [ctypes.c_void_p])
+_sig("mfa_kernel_attribute_count", ctypes.c_int, [])
 _sig("mfa_operand_buffer_binding", ctypes.c_int, [ctypes.c_int])
 _sig("mfa_attention_descriptor_init", None, [_P(AttentionDescriptor)])
 _sig("mfa_attention_kernel_descriptor", ctypes.c_int,
@@ -535,7 +541,7 @@ def last_launches() -> list[dict]:
     """mfa_last_launches: the kernels this thread launched since the previous call."""
     out = KernelPlan()
     lib.mfa_last_launches(ctypes.byref(out))
-    return out.as_list()
+    return out.as_list(strict=False)
 
 
 class MultiHeadAttention:

@@ -88,10 +88,19 @@ def test_block_head_clamped_to_padded_head():
     assert k.block_head == 8
 
 
-def test_unsupported_head_dimension():
-    d = mfa.AttentionDescriptor.make(64, 64, 300)
-    out = mfa.KernelDescriptor()
-    assert mfa.lib.mfa_attention_kernel_descriptor(ctypes.byref(d), 0, ctypes.byref(out)) == 2
+@pytest.mark.parametrize("D", [257, 300, 384, 512, 1000])
+def test_large_head_dimension_descriptor(D):
+    # The reference's tables fall back to their last row for any D
+    # (AttentionDescriptor+Parameters.swift:44-69); here D > 256 runs the D-blocked kernels,
+    # whose head block is the head-dimension chunk they stream.
+    for prec, chunk in ((None, 64), (mfa.Precision.FP16, 128), (mfa.Precision.BF16, 128)):
+        d = mfa.AttentionDescriptor.make(64, 64, D, low_precision=prec is not None, precision=prec)
+        for kind in (mfa.KernelType.forward, mfa.KernelType.backwardQuery,
+                     mfa.KernelType.backwardKeyValue):
+            k = mfa.kernel_descriptor(d, kind)
+            assert k.block_head == chunk and k.head_dimension == D
+            kern = mfa.attention_kernel(k)
+            assert b"bigd" in kern.variant, kern.variant
 
 
 def test_broadcast_compatibility_rules():

@@ -83,15 +83,20 @@ def test_mla_forward_small(gpu, prec, causal):
     assert maxerr(o, ref["O"]) < (5e-2 if prec == P.FP16 else 1e-1)
 
 
-def test_mla_config4_one_head(gpu):
-    # BASELINE.json configs[3]: latent 512 -> D 128, bf16, S4096 (H16 assumed).
+def test_mla_config4_heads(gpu):
+    # BASELINE.json configs[3]: latent 512 -> D 128, bf16, S4096 (H16 assumed).  The
+    # decompression is an fp32-accumulated GEMM rounded once to bf16, so it must agree with the
+    # oracle's GEMM rounded the same way to within a few bf16 ulps (relL2 <= 5e-3; a wrong
+    # k-loop tail would show as ~1e-1).  Attention is held to the oracle on the ORACLE's
+    # decompressed K/V (not the GPU's), heads 0, 7, 15.
     B, H, S, D, latent = 1, 16, 4096, 128, 512
     o, l, kb, vb, Q, Kd, Vd, to_bhsd = run_mla(B, H, S, D, latent, P.BF16, seed=4)
-    assert relerr(kb, Kd) < 2e-2 and relerr(vb, Vd) < 2e-2
+    rk, rv = relerr(kb, Kd), relerr(vb, Vd)
+    print(f"C4 decompression relL2: K {rk:.2e} V {rv:.2e}")
+    assert rk <= 5e-3 and rv <= 5e-3
     on = o.cpu().numpy()
     assert np.isfinite(on).all()
-    h = 3
-    Kh = to_bhsd(kb.float().cpu().numpy())[:, h:h + 1]
-    Vh = to_bhsd(vb.float().cpu().numpy())[:, h:h + 1]
-    ref = ol.attention(Q[:, h:h + 1], Kh, Vh)
-    assert maxerr(on[:, h:h + 1], ref["O"]) < 2e-2
+    Kb, Vb = to_bhsd(Kd), to_bhsd(Vd)
+    for h in (0, 7, 15):
+        ref = ol.attention(Q[:, h:h + 1], Kb[:, h:h + 1], Vb[:, h:h + 1])
+        assert maxerr(on[:, h:h + 1], ref["O"]) < 2e-2, h

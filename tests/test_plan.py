@@ -175,39 +175,69 @@ def test_custom_mismatch_rejected_by_the_call():
         mfa.multihead_plan(d)
 
 
-# transposed O and transposed gradients are rejected, not silently written dense.
-def test_transposed_o_rejected():
-    base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16,
-                                        transpose=(False, False, False, True))
+# transposeState (AttentionDescriptor.swift:150-165): O -> O and dO, Q/K/V -> dQ/dK/dV.  Every
+# transpose is honoured; strided operands and outputs run the generic kernels.
+@pytest.mark.parametrize("tr", [(False, False, False, True), (True, True, True, False),
+                                (True, True, True, True), (False, True, False, True)])
+def test_transposes_accepted_on_generic_kernels(tr):
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16, transpose=tr)
     d = mfa.MultiHeadDescriptor.make(base, 1, 2, 128, 64)
+    assert one(mfa.multihead_plan(d))["name"].startswith("mfa_fwd_kernel<")
+    assert one(mfa.multihead_plan(d, K.backwardQuery))["name"].startswith("mfa_bwd_q_kernel<")
+    assert one(mfa.multihead_plan(d, K.backwardKeyValue))["name"].startswith("mfa_bwd_kv_kernel<")
+    full = mfa.AttentionDescriptor.make(128, 128, 64, transpose=tr)
     for kind in (K.forward, K.backwardQuery, K.backwardKeyValue):
-        with pytest.raises(mfa.MFAError) as e:
-            mfa.multihead_plan(d, kind)
-        assert e.value.status == 2
+        kd = mfa.kernel_descriptor(full, kind)
+        assert kd.transpose_state[int(mfa.Operand.O)] == tr[3]
+        assert kd.transpose_state[int(mfa.Operand.dO)] == tr[3]
+        assert kd.transpose_state[int(mfa.Operand.dQ)] == tr[0]
+        assert kd.transpose_state[int(mfa.Operand.dK)] == tr[1]
+        assert kd.transpose_state[int(mfa.Operand.dV)] == tr[2]
 
 
-def test_transposed_qkv_forward_only():
-    base = mfa.AttentionDescriptor.make(low_precision=True, precision=P.FP16,
-                                        transpose=(True, True, True, False))
-    d = mfa.MultiHeadDescriptor.make(base, 1, 2, 128, 64)
-    assert one(mfa.multihead_plan(d))["name"].startswith("mfa_fwd_kernel<")  # strided operands
-    for kind in (K.backwardQuery, K.backwardKeyValue):
-        with pytest.raises(mfa.MFAError) as e:
-            mfa.multihead_plan(d, kind)
-        assert e.value.status == 2
-    full = mfa.AttentionDescriptor.make(128, 128, 64, transpose=(True, False, False, False))
-    mfa.kernel_descriptor(full, K.forward)
-    with pytest.raises(mfa.MFAError):
-        mfa.kernel_descriptor(full, K.backwardQuery)
-
-
-def test_quantized_rejects_transposes():
+def test_quantized_transposes_accepted():
     base = mfa.AttentionDescriptor.make(256, 256, 128, low_precision=True, precision=P.FP16,
-                                        transpose=(False, True, False, False))
+                                        transpose=(False, True, False, True))
     qd = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=2)
-    with pytest.raises(mfa.MFAError) as e:
-        mfa.quantized_plan(qd)
-    assert e.value.status == 2
+    names = [r["name"] for r in mfa.quantized_plan(qd)]
+    assert names[-1].startswith("mfa_fwd_kernel<")  # transposed O: generic kernel
+
+
+@pytest.mark.parametrize("D", [288, 320, 384, 512, 1024])
+@pytest.mark.parametrize("prec,tag", [(P.FP32, "Arith32<64>, 64"), (P.FP16, "Arith16<F16, 128>, 128"),
+                                      (P.BF16, "Arith16<BF16, 128>, 128")])
+def test_large_head_dimension_plan(D, prec, tag):
+    lp = prec != P.FP32
+    base = mfa.AttentionDescriptor.make(low_precision=lp, precision=prec if lp else None,
+                                        causal=True)
+    d = mfa.MultiHeadDescriptor.make(base, 2, 3, 300, D)
+    f = one(mfa.multihead_plan(d))
+    assert f["name"] == f"mfa_fwd_bigd_kernel<{tag}>"
+    nob = -(-D // (64 if prec == P.FP32 else 128))
+    assert f["workgroups"] == 3 * 2 * 3 * nob  # 128-row blocks x B x H x output slices
+    q = one(mfa.multihead_plan(d, K.backwardQuery))
+    kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
+    assert q["name"].startswith("mfa_bwd_q_bigd_kernel<" + tag)
+    assert kv["name"].startswith("mfa_bwd_kv_bigd_kernel<" + tag)
+
+
+def test_large_head_dimension_quantized_plan():
+    # INT8 K/V at D = 384: one dequantisation pass per operand, then the D-blocked forward,
+    # whatever the number of query rows (decode shapes included).
+    for R in (1, 512):
+        base = mfa.AttentionDescriptor.make(R, 1024, 384, low_precision=True, precision=P.FP16)
+        qd = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=2)
+        names = [r["name"] for r in mfa.quantized_plan(qd)]
+        assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2, names
+        assert names[2].startswith("mfa_fwd_bigd_kernel<Arith16<F16, 128>")
+
+
+def test_absorbed_mla_rejects_transposes():
+    d = mla_desc(1, 2, 64, 64, 64, 256)
+    d.base.transpose_q = 1
+    p = 0x100000
+    st = mfa.lib.mfa_mla_forward_absorbed(ctypes.byref(d), p, p, p, p, None, p, None, None)
+    assert st == 2
 
 
 def mla_desc(B, H, Sq, Skv, D, Lat):
