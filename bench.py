@@ -206,6 +206,42 @@ def main():
         }
         del qf, kf, vf, o3, l3, kq, vq, kh, vh, k4, v4
 
+        # INT8 K/V decode (the KV-cache shape INT8 K/V exists for): B32 H16, 8192 cached keys,
+        # 1 and 16 query rows per head; HBM-bound on the INT8 K/V read (2·D bytes per key).
+        Bd, Hd, Cd, Dd = 32, 16, 8192, 128
+        kd8 = torch.randint(0, 256, (Bd, Hd, Cd, Dd), dtype=torch.uint8, device=dev, generator=g)
+        vd8 = torch.randint(0, 256, (Bd, Hd, Cd, Dd), dtype=torch.uint8, device=dev, generator=g)
+        tkd = mfa.quantized_tensor(kd8, mfa.Precision.INT8, scale=0.25 / 127)
+        tvd = mfa.quantized_tensor(vd8, mfa.Precision.INT8, scale=0.25 / 127)
+        dec = {}
+        for Rd in (1, 16):
+            qd8 = uniform((Bd, Hd, Rd, Dd), torch.float16)
+            od8 = torch.empty((Bd, Hd, Rd, Dd), dtype=torch.float32, device=dev)
+            ld8 = torch.empty((Bd, Hd, Rd), dtype=torch.float16, device=dev)
+            based = mfa.AttentionDescriptor.make(Rd, Cd, Dd, low_precision=True,
+                                                 precision=mfa.Precision.FP16)
+            qdd = mfa.quantized_descriptor(based, mfa.Precision.FP16, mfa.Precision.INT8,
+                                           mfa.Precision.INT8, B=Bd, H=Hd)
+            tqd = mfa.quantized_tensor(qd8, mfa.Precision.FP16)
+            msd = ev_time(lambda: qa.forward(qdd, tqd, tkd, tvd, od8, ld8, stream=stream))
+            kv_bytes = 2 * Bd * Hd * Cd * Dd
+            io_bytes = kv_bytes + qd8.numel() * 2 + od8.numel() * 4 + ld8.numel() * 2
+            dec[f"s_q{Rd}"] = {
+                "ms": round(msd, 4),
+                "GBps": round(io_bytes / msd / 1e6, 1),
+                "hbm_frac": round(io_bytes / msd / 1e6 / 8000.0, 4),
+                "kernels": [r["name"] for r in mfa.quantized_plan(qdd, mfa.KernelType.forward,
+                                                                   tqd, tkd, tvd)],
+            }
+            del qd8, od8, ld8
+        result["int8_decode"] = {
+            "workload": f"QuantizedAttention forward, INT8 K/V (per-tensor) + fp16 Q, B{Bd} H{Hd} "
+                        f"S_kv {Cd} D{Dd}, S_q 1 and 16 (decode / KV cache), non-causal",
+            "bytes": "INT8 K + V once, plus Q (fp16), O (fp32) and L (fp16); roof 8 TB/s HBM",
+            **dec,
+        }
+        del kd8, vd8
+
     # ---------------------------------------------------------------- C5: fwd + bwd, D=256
     if not args.no_c5:
         B5, H5, S5, D5 = args.c5_batch, 32, 4096, 256

@@ -1,0 +1,308 @@
+// attention_decode.hip — split-KV forward for INT8 K/V with few query rows per kv head
+// (decode / KV-cache shapes): QuantizedAttention.forward (QuantizedAttention.swift:135-263)
+// with the reference's dequantise-on-load semantics (GEMMHeaders.swift:679-738): every K/V
+// element enters the product as (q - zp) exactly, the per-tensor scales folded into the
+// softmax and output multipliers, as in the other dequant-exact kernels.
+//
+// A decode step reads the whole K/V cache to serve 1-16 query rows per head, so the kernel is
+// HBM-bound: 2·D bytes per key.  Layout of the work:
+//   * unit = (batch, kv head, 32-row tile of the kv group's query rows); the group's rows
+//     (H/H_kv query heads x R rows) share every K/V byte, so a tile reads them once;
+//   * each unit's keys are split over `nsplit` workgroups of 4 waves; inside a workgroup the
+//     waves take 32-key tiles round-robin, each wave with its own 2-slot LDS ring filled by
+//     LDS-DMA of the INT8 bytes (1 KiB per wave-instruction; no staging registers, no
+//     barriers: a wave waits for its own DMA with a counted vmcnt);
+//   * S^T = K·Q^T on v_mfma_f32_32x32x16 with K fragments widened from INT8 in registers
+//     (the exact fp16 magic-number conversion of mfa_stage.h); online softmax per wave; V^T
+//     fragments read transposed from the INT8 tile (ds_read_b64_tr_b8) and widened the same
+//     way for O^T += V^T·P^T;
+//   * every wave writes its partial (m, l, unnormalised O) for the valid rows; a merge pass
+//     combines the 4·nsplit partials of each row into O = Σ w_s O_s / Σ w_s l_s and
+//     L = m + log2 l (w_s = exp2(m_s - m)).
+#include "mfa_stage.h"
+#include "mfa_dispatch.h"
+
+namespace mfa {
+
+typedef int i32x2d __attribute__((ext_vector_type(2)));
+
+template <class E>
+__device__ __forceinline__ i16x8 widen_i8(uint32_t lo, uint32_t hi, float zp) {
+  return __builtin_bit_cast(i16x8, dequant_fast<E, SRC_I8>(make_uint4(lo, hi, 0u, 0u), zp));
+}
+
+template <class E, int DP>
+__global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(DecodeParams dp) {
+  const FwdParams& p = dp.f;
+  constexpr int BK = 32, NSLOT = 2, ND = DP / 32;
+  constexpr int ROWB = DP;                  // INT8: one byte per element
+  using T = Tile16<ROWB / 2>;               // [BK][ROWB bytes], 16-byte chunks XOR-swizzled
+  constexpr int TILEB = BK * ROWB;          // one K or V tile
+  constexpr int NPC = TILEB / 1024;         // 1-KiB DMA pieces per tile
+  constexpr int RP = 1024 / ROWB;           // rows per piece
+  static_assert(NPC >= 1 && NPC <= 8, "decode tile geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  char* const ring = smem + wave * (NSLOT * 2 * TILEB);  // slot s: K at 2s·TILEB, V after it
+
+  const int split = blockIdx.x;
+  const int u = blockIdx.y + gridDim.y * blockIdx.z;    // (b·H_kv + kvh)·nrt + rt
+  const int rt = u % dp.nrt;
+  const int bk = u / dp.nrt;
+  const int kvh = bk % p.Hkv, b = bk / p.Hkv;
+  const float c = p.c_log2;
+
+  // The lane's query row of this tile: row = g·R + q of kv head kvh's group (h = kvh + g·H_kv).
+  const int row = rt * 32 + l32;
+  const bool rvalid = row < dp.rows;
+  i16x8 qf[DP / 16];
+  {
+    const int g = rvalid ? row / p.R : 0, q = rvalid ? row % p.R : 0;
+    const int h = kvh + g * p.Hkv;
+    const uint16_t* qrow =
+        (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh + (int64_t)q * p.q.ss;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
+      const int d0 = 16 * s + 8 * hh;
+      i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (rvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
+      qf[s] = v;
+    }
+  }
+
+  // Keys of this split: [k0, k1); this wave's tiles k0 + 32·(wave + 4i).
+  const int k0 = split * dp.chunk;
+  const int k1 = min(p.C, k0 + dp.chunk);
+  const int nt = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
+  const int mine = nt > wave ? (nt - wave + 3) / 4 : 0;
+
+  // LDS-DMA of one 32-row tile: piece n holds rows n·RP .. n·RP + RP - 1 (Tile16 rows are
+  // contiguous); lane l lands at byte 16·l of it = row n·RP + l / CPR, physical chunk l % CPR,
+  // so it fetches logical chunk (l % CPR) ^ swz(row).  Rows past C and chunks past D read as
+  // zeros (range-checked descriptor per piece, out-of-row chunks out of range).
+  constexpr int CPR = ROWB / 16;
+  int poff[NPC];
+#pragma unroll
+  for (int n = 0; n < NPC; ++n) {
+    const int r = n * RP + lane / CPR;
+    const int ch = (lane % CPR) ^ T::swz(r);
+    poff[n] = ch * 16 < p.D ? r * (int)p.k.ss + ch * 16 : 0x40000000;
+  }
+  const char* khead = (const char*)p.k.ptr + (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
+  const char* vhead = (const char*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
+  const int kbytes = (int)((int64_t)(p.C - 1) * p.k.ss + p.D);
+  const int vbytes = (int)((int64_t)(p.C - 1) * p.v.ss + p.D);
+  auto issue = [&](int i, int slot) {
+    const int t = k0 + BK * (wave + 4 * i);
+    char* kdst = ring + slot * 2 * TILEB;
+#pragma unroll
+    for (int n = 0; n < NPC; ++n) {
+      const int rk = t * (int)p.k.ss;
+      lds_dma16(khead + rk, max(kbytes - rk, 0), poff[n], kdst + n * 1024);
+    }
+#pragma unroll
+    for (int n = 0; n < NPC; ++n) {
+      const int rv = t * (int)p.v.ss;
+      // V rows share the K piece geometry when the row strides agree (host-checked).
+      lds_dma16(vhead + rv, max(vbytes - rv, 0), poff[n], kdst + TILEB + n * 1024);
+    }
+  };
+
+  // ds_read_b64_tr_b8 lanes (see attention_fwd_i8.hip): in each 16-lane group, lane 2j supplies
+  // the row of key acc_row(j + 8s, hh) and receives column d0 + (lane & 15) of the 8 rows.
+  const int trj = (lane & 15) >> 1;
+  const int trg = (lane >> 4) & 1;
+  const int trow0 = acc_row(trj, hh), trow1 = acc_row(trj + 8, hh);
+  const float zk = (float)p.k.zp, zv = (float)p.v.zp;
+
+  f32x16 o[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) o[dt] = zero16();
+  float m = -kFltMax, lh = 0.f;
+
+  if (mine > 0) issue(0, 0);
+  for (int i = 0; i < mine; ++i) {
+    const int slot = i & 1;
+    if (i + 1 < mine) {
+      issue(i + 1, slot ^ 1);
+      __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NPC));  // tile i landed, tile i+1 in flight
+    } else {
+      wait_vm();
+    }
+    const char* kt = ring + slot * 2 * TILEB;
+    const char* vt = kt + TILEB;
+    const int t = k0 + BK * (wave + 4 * i);
+
+    // S^T = K·Q^T: key l32 on the A operand's row, elements d = 16s + 8hh + j.
+    f32x16 sa[1];
+    sa[0] = zero16();
+#pragma unroll
+    for (int st = 0; st < DP / 16; ++st) {
+      const uint2 kb = *reinterpret_cast<const uint2*>(kt + T::off(l32, st) + 8 * hh);
+      sa[0] = E::mma(widen_i8<E>(kb.x, kb.y, zk), qf[st], sa[0]);
+    }
+    if (t + BK > p.C) {
+      // Keys past C: -inf (key offset acc_row(r, hh) within the tile).
+      mask_outside<1>(sa, -0x40000000, p.C - t - 4 * hh - 1, -__builtin_inff());
+    }
+    f32x16& s = sa[0];
+    float mx = s[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
+    mx = cross_half_max(mx) * c;
+    if (__any(mx > m)) {
+      const float m_new = fmaxf(m, mx);
+      const float corr = __builtin_amdgcn_exp2f(m - m_new);
+      m = m_new;
+      lh *= corr;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= corr;
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], c, -m));
+      s[r] = pv;
+      rs += pv;
+    }
+    lh += rs;
+    i16x8 pb[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[ks][j] = (short)E::from_f32(s[8 * ks + j]);
+    // O^T += V^T·P^T.
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int col = dt * 32 + 16 * trg + 8 * (lane & 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const char* pa = vt + T::off(ks ? trow1 : trow0, col >> 4) + (col & 15);
+        const i32x2d w = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+            (__attribute__((address_space(3))) i32x2d*)pa);
+        o[dt] = E::mma(widen_i8<E>((uint32_t)w[0], (uint32_t)w[1], zv), pb[ks], o[dt]);
+      }
+    }
+  }
+
+  // This wave's partial for the tile's valid rows.
+  const float l = cross_half_sum(lh);
+  if (rvalid) {
+    const int np = dp.nsplit * 4;
+    const int64_t pidx = ((int64_t)u * np + split * 4 + wave) * 32 + l32;
+    float* orow = dp.opart + pidx * p.D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        if (d < p.D)
+          *reinterpret_cast<float4*>(orow + d) =
+              make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
+      }
+    if (hh == 0) dp.mlpart[pidx] = make_float2(m, l);
+  }
+}
+
+// One query row per wave: combines the row's 4·nsplit partials.  O is written with the
+// caller's strides, L = m + log2 l in the descriptor's memory precision.
+__global__ void __launch_bounds__(256) mfa_decode_merge_kernel(DecodeParams dp) {
+  const FwdParams& p = dp.f;
+  const int lane = threadIdx.x & 63;
+  const int64_t rid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (b·H + h)·R + q
+  if (rid >= (int64_t)p.B * p.H * p.R) return;
+  const int q = (int)(rid % p.R);
+  const int bh = (int)(rid / p.R);
+  const int h = bh % p.H, b = bh / p.H;
+  const int kvh = h % p.Hkv, g = h / p.Hkv;
+  const int row = g * p.R + q;
+  const int u = (b * p.Hkv + kvh) * dp.nrt + row / 32;
+  const int np = dp.nsplit * 4;
+  const int64_t base = (int64_t)u * np * 32 + (row % 32);
+  float mx = -kFltMax;
+  for (int s = 0; s < np; ++s) mx = fmaxf(mx, dp.mlpart[base + (int64_t)s * 32].x);
+  float l = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int d = 4 * lane;
+  for (int s = 0; s < np; ++s) {
+    const float2 ml = dp.mlpart[base + (int64_t)s * 32];
+    const float w = __builtin_amdgcn_exp2f(ml.x - mx);
+    l += ml.y * w;
+    if (d < p.D) {
+      const float4 v = *reinterpret_cast<const float4*>(dp.opart + (base + (int64_t)s * 32) * p.D + d);
+      acc.x += v.x * w; acc.y += v.y * w; acc.z += v.z * w; acc.w += v.w * w;
+    }
+  }
+  l += kFltMin;
+  const float inv = p.o_mul / l;
+  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
+  const float vals[4] = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (d + e < p.D) orow[(int64_t)(d + e) * p.o_sd] = vals[e];
+  if (lane == 0) {
+    const float L = mx + __log2f(l);
+    const int64_t li = (int64_t)(b * p.H + h) * p.R + q;
+    if (p.l_f16)
+      reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+    else
+      reinterpret_cast<float*>(p.l)[li] = L;
+  }
+}
+
+// Split of the key range: enough workgroups for two per CU (512) when the units alone do not
+// provide them, each wave at least 4 tiles (128 keys).
+void decode_layout(int B, int Hkv, int rows, int C, int* nrt, int* nsplit, int* chunk) {
+  *nrt = (rows + 31) / 32;
+  const int units = B * Hkv * *nrt;
+  const int tiles = (C + 31) / 32;
+  int ns = (512 + units - 1) / units;
+  if (ns > tiles / 16) ns = tiles / 16;
+  if (ns < 1) ns = 1;
+  const int per = (tiles + ns - 1) / ns;  // tiles per split, rounded to whole 4-wave rounds
+  *chunk = ((per + 3) / 4) * 4 * 32;
+  *nsplit = (C + *chunk - 1) / *chunk;
+}
+
+size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D) {
+  int nrt, ns, chunk;
+  decode_layout(B, Hkv, rows, C, &nrt, &ns, &chunk);
+  const size_t parts = (size_t)B * Hkv * nrt * ns * 4 * 32;
+  return parts * D * 4 + parts * 8 + 256;
+}
+
+hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hipStream_t stream) {
+  if (p.k.prec != P_INT8 || p.v.prec != P_INT8 || p.k.ss != p.v.ss) return hipErrorNotSupported;
+  DecodeParams dp;
+  dp.f = p;
+  dp.rows = (p.H / p.Hkv) * p.R;
+  decode_layout(p.B, p.Hkv, dp.rows, p.C, &dp.nrt, &dp.nsplit, &dp.chunk);
+  const size_t parts = (size_t)p.B * p.Hkv * dp.nrt * dp.nsplit * 4 * 32;
+  dp.opart = (float*)workspace;
+  dp.mlpart = (float2*)((char*)workspace + ((parts * p.D * 4 + 255) & ~(size_t)255));
+  const int units = p.B * p.Hkv * dp.nrt;
+  if (units >= 65536) return hipErrorNotSupported;
+  const dim3 grid(dp.nsplit, units, 1);
+  const int DP = p.D <= 64 ? 64 : p.D <= 128 ? 128 : 256;
+  hipError_t e = hipErrorNotSupported;
+#define MFA_DEC(ELEM, EE, DPV)                                                                 \
+  if (elem == ELEM && DP == DPV)                                                               \
+    e = launch(mfa_fwd_decode_kernel<EE, DPV>, grid, dim3(256), 4 * 2 * 2 * 32 * DPV, stream, dp);
+  MFA_DEC(P_FP16, F16, 64)
+  MFA_DEC(P_FP16, F16, 128)
+  MFA_DEC(P_FP16, F16, 256)
+  MFA_DEC(P_BF16, BF16, 64)
+  MFA_DEC(P_BF16, BF16, 128)
+  MFA_DEC(P_BF16, BF16, 256)
+#undef MFA_DEC
+  if (e != hipSuccess) return e;
+  const int64_t nrows = (int64_t)p.B * p.H * p.R;
+  return launch(mfa_decode_merge_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, stream, dp);
+}
+
+}  // namespace mfa

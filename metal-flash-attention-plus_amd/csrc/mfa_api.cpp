@@ -674,6 +674,25 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
          ((uintptr_t)p.v.ptr % 4 == 0);
 }
 
+// The split-KV decode kernel (attention_decode.hip): FP16/BF16 Q, per-tensor INT8 K/V with
+// the same row layout, 16-byte rows, D % 16 == 0, D <= 256, no mask, dense O rows.
+bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
+  if (const char* e = getenv("MFA_DECODE")) {
+    if (e[0] == '0') return false;
+  }
+  if (elem != 1 && elem != 2) return false;
+  if (is_quantized(qp) || kp != MFA_PRECISION_INT8 || vp != MFA_PRECISION_INT8) return false;
+  if (p.k.bscale || p.v.bscale) return false;
+  if (p.D % 16 != 0 || p.D > 256 || p.C <= 0 || !(p.c_log2 > 0.f)) return false;
+  if (p.mask.causal || p.mask.window || p.mask.amask || p.mask.ranges) return false;
+  if (p.q.sd != 1 || !p.q.vec || p.k.sd != 1 || p.v.sd != 1) return false;
+  if (p.k.ss != p.v.ss || p.k.ss % 16 || p.k.sh % 16 || p.k.sb % 16 || p.v.sh % 16 ||
+      p.v.sb % 16)
+    return false;
+  if ((uintptr_t)p.k.ptr % 16 || (uintptr_t)p.v.ptr % 16) return false;
+  return (int64_t)p.C * p.k.ss < ((int64_t)1 << 31);
+}
+
 // Quantised operands go through one dequantisation pass into a dense 16-bit copy
 // (kv_dequant.hip) when the compute type is 16-bit, D % 8 == 0 and each kv head serves at
 // least 128 query rows: every element is then converted once per call instead of once per
@@ -778,6 +797,18 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     pi.nblk = (R + 127) / 128;
     return hip_status(mfa::fwd_i8mma_dispatch(pi, elem, (hipStream_t)stream),
                       "mfa_fwd (integer matmul) launch");
+  }
+  if (decode_eligible(p, elem, qp, kp, vp) && !dequant_pass_worth(R, H, Hkv, D, elem)) {
+    // Decode / KV-cache shapes: split-KV kernel reading the INT8 bytes (attention_decode.hip).
+    void* ws = nullptr;
+    if (mfa::plan_capture()) {
+      ws = (void*)kPlanDummy;
+    } else if ((st = scratch(mfa::decode_workspace_bytes(B, Hkv, (H / Hkv) * R, C, D), &ws, 9,
+                             (hipStream_t)stream)) != MFA_SUCCESS) {
+      return st;
+    }
+    const hipError_t e = mfa::fwd_decode_dispatch(p, elem, ws, (hipStream_t)stream);
+    if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (decode) launch");
   }
   int kvsrc = src_kind(kp);
   if (dequant_pass_worth(R, H, Hkv, D, elem)) {

@@ -67,6 +67,17 @@ struct BwdParams {
   MaskArgs mask;
 };
 
+// Split-KV decode forward (attention_decode.hip): INT8 K/V, few query rows per kv head.
+struct DecodeParams {
+  FwdParams f;
+  int32_t rows;      // query rows per kv head: (H / H_kv) · R
+  int32_t nrt;       // 32-row tiles per kv head
+  int32_t nsplit;    // key splits per unit (unit = batch, kv head, row tile)
+  int32_t chunk;     // keys per split (whole rounds of 4 waves x 32-key tiles)
+  float* opart;      // [units][4·nsplit][32][D] unnormalised O of each wave
+  float2* mlpart;    // [units][4·nsplit][32] (m, l)
+};
+
 // MFMA GEMM (gemm.hip): C = A·B (+C); two (B, C) pairs share A when b[1] != nullptr.
 struct GemmParams {
   const void* a;

@@ -474,3 +474,61 @@ def test_integer_matmul_c3_heads(gpu):
         ref = ol.attention(deq["Q"][:, h:h + 1], deq["K"][:, h:h + 1], deq["V"][:, h:h + 1])
         assert relerr(on[:, h:h + 1], ref["O"]) < I8MM_REL, h
         assert maxerr(ln[:, h:h + 1], ref["L"]) < I8MM_L, h
+
+
+# ----------------------------------------------------------------------- split-KV decode
+# Few query rows per kv head (R·H/H_kv < 128) with per-tensor INT8 K/V run the split-KV decode
+# kernel (attention_decode.hip): the INT8 bytes are staged by LDS-DMA and widened in registers
+# (dequant-exact), partials of every wave merged by a second pass.  Held to the oracle on the
+# dequantised values at the dequant-exact tolerance, and to the previous (generic) path.
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,qp", [
+    (2, 4, 4, 1, 1000, 128, P.FP16),
+    (1, 4, 4, 16, 4101, 128, P.FP16),
+    (1, 8, 2, 3, 777, 64, P.BF16),     # GQA: 12 rows per kv head
+    (2, 4, 1, 5, 300, 256, P.FP16),    # MQA: 20 rows, D 256
+    (1, 16, 1, 4, 2048, 128, P.BF16),  # 64 rows per kv head: two row tiles
+    (1, 2, 2, 1, 33, 64, P.FP16),      # one partial tile
+])
+def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
+    rng = np.random.default_rng(R * 13 + C)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, P.INT8, P.INT8, B=B, H=H, Hkv=Hkv)
+    names = [r["name"] for r in mfa.quantized_plan(desc)]
+    assert names[0].startswith("mfa_fwd_decode_kernel<") and names[1] == "mfa_decode_merge_kernel", names
+    o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"])
+    assert np.isfinite(o.cpu().numpy()).all()
+    assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
+    assert maxerr(l, ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max()
+    monkeypatch.setenv("MFA_DECODE", "0")
+    o2, _, _, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
+    monkeypatch.delenv("MFA_DECODE")
+    assert maxerr(o, o2.cpu().numpy()) < 2e-3
+
+
+def test_decode_nonzero_zero_point(gpu):
+    # Per-tensor zero points ride into the widening as (q - zp), exactly.
+    B, H, R, C, D = 1, 2, 2, 500, 128
+    rng = np.random.default_rng(5)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    kq = rng.integers(-100, 100, (B, H, C, D)).astype(np.int8)
+    vq = rng.integers(-100, 100, (B, H, C, D)).astype(np.int8)
+    ks, vs, kz, vz = 0.02, 0.03, 7, -5
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=P.FP16)
+    desc = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=B, H=H)
+    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
+    tk = mfa.quantized_tensor(kt, P.INT8, scale=ks, zero_point=kz)
+    tv = mfa.quantized_tensor(vt, P.INT8, scale=vs, zero_point=vz)
+    o = torch.empty((B, H, R, D), dtype=torch.float32, device=DEV)
+    l = torch.empty((B, H, R), dtype=torch.float16, device=DEV)
+    assert mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)[0]["name"].startswith(
+        "mfa_fwd_decode_kernel<")
+    mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+    torch.cuda.synchronize()
+    Kd = (kq.astype(np.float32) - kz) * np.float32(ks)
+    Vd = (vq.astype(np.float32) - vz) * np.float32(vs)
+    ref = ol.attention(seen(Q, P.FP16), Kd, Vd)
+    assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
