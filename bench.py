@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true")
     ap.add_argument("--no-mla", action="store_true")
+    ap.add_argument("--no-sparse", action="store_true", help="skip the block-sparse row")
     ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8(f) rows")
     ap.add_argument("--c5-batch", type=int, default=8)
     ap.add_argument("--fake-device", action="store_true",
@@ -352,6 +353,47 @@ def main():
             "ms_per_step": round(el4 / n4 * 1e3, 4),
         }
         del lat, wk, wv, q4, o4, kb4, vb4
+
+    # ------------------------------------------- sparse ranges (block-sparse) on the tuned path
+    if not args.no_sparse:
+        import numpy as np
+        Hs, Ss, Ds, blk, band = 16, 4096, 128, 128, 8
+        nb = Ss // blk
+        pat = np.zeros((nb, nb), dtype=np.uint8)
+        for i in range(nb):  # a band of `band` key blocks around the diagonal
+            c0 = min(max(0, i - band // 2), nb - band)
+            pat[i, c0:c0 + band] = 1
+        rb = np.zeros((nb, 2), dtype=np.uint32)
+        mfa.lib.mfa_sparse_build_block_sparse(pat.ctypes.data, nb, nb, blk, rb.ctypes.data)
+        rows = np.ascontiguousarray(np.broadcast_to(np.repeat(rb, blk, axis=0), (B, Hs, Ss, 2)))
+        mask_s = torch.from_numpy(rows.view(np.int32)).to(dev)
+        qs, ks_, vs_ = (uniform((B, Hs, Ss, Ds), torch.float16) for _ in range(3))
+        os_ = torch.empty((B, Hs, Ss, Ds), dtype=torch.float32, device=dev)
+        ls = torch.empty((B, Hs, Ss), dtype=torch.float16, device=dev)
+        base_s = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16,
+                                              sparse_mask=mfa.MaskType.sparseRanges)
+        desc_s = mfa.MultiHeadDescriptor.make(base_s, B, Hs, Ss, Ds)
+        base_d = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16)
+        desc_d = mfa.MultiHeadDescriptor.make(base_d, B, Hs, Ss, Ds)
+        ms_sp = ev_time(lambda: mha.forward(desc_s, qs, ks_, vs_, os_, ls, mask=mask_s,
+                                            stream=stream))
+        mfa.last_launches()
+        mha.forward(desc_s, qs, ks_, vs_, os_, ls, mask=mask_s, stream=stream)
+        plan_s = [r["name"] for r in mfa.last_launches()]
+        ms_dn = ev_time(lambda: mha.forward(desc_d, qs, ks_, vs_, os_, ls, stream=stream))
+        pairs = int((rows[0, 0, :, 1].astype(np.int64) - rows[0, 0, :, 0]).sum()) * B * Hs
+        fs = 4.0 * Ds * pairs
+        result["block_sparse"] = {
+            "workload": f"sparse ranges from buildBlockSparse, fp16 B{B} H{Hs} S{Ss} D{Ds}, "
+                        f"{blk}x{blk} blocks, band of {band} key blocks per row block "
+                        f"(density {band / nb:.3f})",
+            "tflops_on_kept_pairs": round(fs / (ms_sp * 1e-3) / 1e12, 2),
+            "roofline_frac": round(fs / (ms_sp * 1e-3) / 1e12 / PEAK_FP16_TFLOPS, 4),
+            "ms": round(ms_sp, 4), "dense_ms": round(ms_dn, 4),
+            "speedup_vs_dense": round(ms_dn / ms_sp, 2),
+            "kernels": plan_s,
+        }
+        del qs, ks_, vs_, os_, ls, mask_s
 
     # ------------------------------------------------- SURVEY §8(f) rows (one GPU's view)
     if not args.no_next:

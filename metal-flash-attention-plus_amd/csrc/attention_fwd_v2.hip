@@ -22,319 +22,9 @@
 //     −inf give the same P (exactly 0) and the same O and L.
 // Lazy rescaling (threshold 8 in log2 units, cdna_hip_programming.md T13) is kept: the running
 // max and the −m tile change only when a tile's max exceeds m + 8.
-#include <type_traits>
-
-#include "mfa_stage.h"
-#include "mfa_dispatch.h"
+#include "attention_fwd2.h"
 
 namespace mfa {
-
-// Diagnostic build only (tools/diag/fwd_stamps.hip defines MFA_STAMPS): per-wave s_memrealtime
-// stamps (100 MHz) at phase boundaries, into a buffer no kernel output is computed from.
-#ifdef MFA_STAMPS
-__device__ unsigned long long g_mfa_stamps[1 << 20];
-#define MFA_STAMP(slot)                                                                     \
-  do {                                                                                      \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
-    if ((threadIdx.x & 63) == 0)                                                            \
-      g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (slot)] = t_; \
-  } while (0)
-#define MFA_STAMP_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-// Shader-cycle counter at the kernel's start (slot 0) and end (slot 1) of each wave: with the
-// s_memrealtime stamps this gives the clock the chip held during the kernel.
-__device__ unsigned long long g_mfa_cyc[1 << 18];
-#define MFA_CYC(slot)                                                                        \
-  do {                                                                                       \
-    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                              \
-    if ((threadIdx.x & 63) == 0)                                                             \
-      g_mfa_cyc[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (slot)] = c_; \
-  } while (0)
-// Shader-cycle phase totals (slots 5..7 of the wave's record).
-#define MFA_ACC_DECL() unsigned long long acc_[3] = {0, 0, 0}, acct_ = __builtin_amdgcn_s_memtime()
-#define MFA_ACC(k)                                                  \
-  do {                                                              \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
-    acc_[k] += t_ - acct_;                                          \
-    acct_ = t_;                                                     \
-  } while (0)
-#define MFA_ACC_END()                                                                      \
-  do {                                                                                     \
-    if ((threadIdx.x & 63) == 0)                                                           \
-      for (int k_ = 0; k_ < 3; ++k_)                                                       \
-        g_mfa_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 5 + k_] = acc_[k_]; \
-  } while (0)
-#else
-#define MFA_CYC(slot) do {} while (0)
-#define MFA_ACC_DECL() do {} while (0)
-#define MFA_ACC(k) do {} while (0)
-#define MFA_ACC_END() do {} while (0)
-#define MFA_STAMP(slot) do {} while (0)
-#define MFA_STAMP_DRAIN() do {} while (0)
-#endif
-
-// Scheduling knobs (development A/B; the defaults are the shipped configuration): fragment
-// read-ahead for the QK^T and PV chains, MFMA-cluster priority, order pinning.
-template <int AHK_ = 4, int AHV_ = 3, bool PRIO_ = false, bool PIN_ = true, bool SPREAD_ = false>
-struct Tune {
-  static constexpr int AHK = AHK_, AHV = AHV_;
-  static constexpr bool PRIO = PRIO_, PIN = PIN_;
-  static constexpr bool SPREAD = SPREAD_;  // next tile's DMA pieces between the QK^T MFMAs
-};
-using TuneDefault = Tune<>;
-
-// Per-wave running state of 32 query rows (one per lane, halves split the head dimension).
-template <int DP>
-struct RowState {
-  f32x16 o[DP / 32];
-  f32x16 negm;   // −moff in every register (fp16 path): the QK^T chain's initial accumulator
-  float m;       // running max (log2 units, reference convention)
-  float moff;    // the max subtracted inside S' (== m once the row has seen an unmasked key)
-  float lh;      // partial row sum of this half-wave's keys
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int dt = 0; dt < DP / 32; ++dt) o[dt] = zero16();
-    negm = zero16();
-    m = -kFltMax;
-    moff = 0.f;
-    lh = 0.f;
-  }
-};
-
-// One BK-key tile for one wave: S^T = K·Q^T (key in registers, query on the lane), masks,
-// online softmax, O^T += V^T·P^T.
-struct NoHook {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-
-// One tile in three parts: fwd2_qk (S^T = K·Q^T; S·c − moff on the fp16 path), fwd2_softmax
-// (masks, online softmax, P packed as the PV B operand) and fwd2_pv (O^T += V^T·P^T).
-// qk_hook(i) runs after QK^T MFMA i (e.g. staging the next tile piece by piece).
-template <class E, int DP, int BK, class TU = TuneDefault, class QKHook = NoHook>
-__device__ __forceinline__ void fwd2_qk(const char* kt, const int (&rbase)[2],
-                                        const i16x8 (&qf)[DP / 16], const RowState<DP>& st,
-                                        f32x16 (&s)[BK / 32], QKHook&& qk_hook = QKHook()) {
-  using A = Arith16<E, DP>;
-  // Pre-scaled Q, S' = S·c − moff from the MFMA (fp16 up to D=128: at D=256 the −m tile's
-  // registers are worth more than the per-element multiply-add, which halves per MFMA there).
-  constexpr bool PS = E::prec == P_FP16 && DP <= 128;
-  constexpr int NJ = BK / 32, DS = DP / 16;
-  constexpr int NM = DS * NJ;
-  constexpr int AH = DP > 128 ? 2 : TU::AHK;
-  i16x8 kf[AH];
-#pragma unroll
-  for (int i = 0; i < AH; ++i) kf[i] = A::read_row_a(kt, rbase, i % NJ, i / NJ);
-  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    const int ds = i / NJ, j = i % NJ;
-    if (ds == 0)
-      s[j] = A::mma(kf[i % AH], qf[0], PS ? st.negm : zero16());
-    else
-      s[j] = A::mma(kf[i % AH], qf[ds], s[j]);
-    if (i + AH < NM) kf[i % AH] = A::read_row_a(kt, rbase, (i + AH) % NJ, (i + AH) / NJ);
-    qk_hook(i);
-    if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
-}
-
-template <class E, int DP, int BK>
-__device__ __forceinline__ void fwd2_softmax(RowState<DP>& st, f32x16 (&s)[BK / 32],
-                                             i16x8 (&pb)[BK / 16], int t, bool mask_tile, int qi,
-                                             const FwdParams& p, float c, int wsz, int hh) {
-  using A = Arith16<E, DP>;
-  constexpr bool PS = E::prec == P_FP16 && DP <= 128;
-  constexpr int NJ = BK / 32, ND = DP / 32;
-  constexpr float THR = 8.0f;
-  if (mask_tile) {
-    MFA_KEEP_BRANCH();
-    // Keys t + 4hh + kk stay for lo <= kk <= hi: below C, at most qi (causal), at least
-    // qi - wsz (window).
-    const int base = t + 4 * hh;
-    int hi = p.C - 1 - base;
-    if (p.mask.causal) hi = min(hi, qi - base);
-    const int lo = p.mask.window ? qi - wsz - base : -0x40000000;
-    mask_outside<NJ>(s, lo, hi, -__builtin_inff());
-  }
-
-  float mx = s[0][0];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[j][i]);
-  mx = cross_half_max(mx);
-  // Tile max in absolute log2 units.
-  const float mt = PS ? mx + st.moff : mx * c;
-  if (__any(mt > st.m + THR)) {
-    MFA_KEEP_BRANCH();
-    const float m_new = fmaxf(st.m, mt);
-    const float corr = __builtin_amdgcn_exp2f(st.m - m_new);
-    st.m = m_new;
-    st.lh *= corr;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) st.o[dt][i] *= corr;
-    if constexpr (PS) {
-      // Rows still at the initial max saw only masked keys (S' = −inf): keep their offset.
-      const float moff_new = m_new > kMaskLevel ? m_new : st.moff;
-      const float shift = moff_new - st.moff;
-      st.moff = moff_new;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[j][i] -= shift;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) st.negm[i] = -moff_new;
-    }
-  }
-  float rs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float x = PS ? s[j][i] : __builtin_fmaf(s[j][i], c, -st.m);
-      const float pv = __builtin_amdgcn_exp2f(x);
-      s[j][i] = pv;
-      rs[i & 3] += pv;
-    }
-  st.lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) pb[j * 2 + ks] = A::pack(s[j], ks);
-}
-
-template <class E, int DP, int BK, class TU = TuneDefault>
-__device__ __forceinline__ void fwd2_pv(const char* vt, const int (&trb)[2],
-                                        const i16x8 (&pb)[BK / 16], RowState<DP>& st) {
-  using A = Arith16<E, DP>;
-  constexpr int NJ = BK / 32, ND = DP / 32;
-  constexpr int NM = NJ * 2 * ND;
-  constexpr int AH = DP > 128 ? 2 : TU::AHV;
-  i16x8 vf[AH];
-#pragma unroll
-  for (int i = 0; i < AH; ++i) {
-    const int jk = i / ND, dt = i % ND;
-    vf[i] = A::read_tr_a(vt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
-  }
-  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    const int jk = i / ND, dt = i % ND;
-    st.o[dt] = A::mma(vf[i % AH], pb[jk], st.o[dt]);
-    if (i + AH < NM) {
-      const int jn = (i + AH) / ND, dn = (i + AH) % ND;
-      vf[i % AH] = A::read_tr_a(vt, trb, (jn >> 1) * 32, jn & 1, dn * 32);
-    }
-    if constexpr (TU::PIN) __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (TU::PRIO) __builtin_amdgcn_s_setprio(0);
-}
-
-template <class E, int DP, int BK, class TU = TuneDefault, class QKHook = NoHook>
-__device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const int (&rbase)[2],
-                                          const int (&trb)[2], const i16x8 (&qf)[DP / 16],
-                                          RowState<DP>& st, int t, bool mask_tile, int qi,
-                                          const FwdParams& p, float c, int wsz, int hh,
-                                          QKHook&& qk_hook = QKHook()) {
-  f32x16 s[BK / 32];
-  i16x8 pb[BK / 16];
-  fwd2_qk<E, DP, BK, TU>(kt, rbase, qf, st, s, qk_hook);
-  fwd2_softmax<E, DP, BK>(st, s, pb, t, mask_tile, qi, p, c, wsz, hh);
-  fwd2_pv<E, DP, BK, TU>(vt, trb, pb, st);
-}
-
-// Q fragments of the lane's query row, pre-scaled by c (rounded to the element type) on the
-// fp16 path.
-// Q fragments in two halves so a caller can issue the loads early and scale them later
-// (the pair kernel overlaps the next block's Q with the current block's merge and stores).
-template <int DP>
-__device__ __forceinline__ void load_q2_raw(i16x8 (&qf)[DP / 16], const FwdParams& p, int b,
-                                            int h, int qi, bool qvalid, int hh) {
-  const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh +
-                         (int64_t)(qvalid ? qi : 0) * p.q.ss;
-#pragma unroll
-  for (int s = 0; s < DP / 16; ++s) {
-    const int d0 = 16 * s + 8 * hh;
-    i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (qvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-    qf[s] = v;
-  }
-}
-
-template <class E, int DP>
-__device__ __forceinline__ void prescale_q2(i16x8 (&qf)[DP / 16], float c) {
-  if constexpr (E::prec == P_FP16 && DP <= 128) {
-#pragma unroll
-    for (int s = 0; s < DP / 16; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = (short)E::from_f32(E::to_f32((uint16_t)qf[s][j]) * c);
-  }
-}
-
-template <class E, int DP>
-__device__ __forceinline__ void load_q2(i16x8 (&qf)[DP / 16], const FwdParams& p, int b, int h,
-                                        int qi, bool qvalid, int hh, float c) {
-  load_q2_raw<DP>(qf, p, b, h, qi, qvalid, hh);
-  prescale_q2<E, DP>(qf, c);
-}
-
-__device__ __forceinline__ void store_l(const FwdParams& p, float L, int b, int h, int qi) {
-  const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
-  if (p.l_f16)
-    reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
-  else
-    reinterpret_cast<float*>(p.l)[li] = L;
-}
-
-// 16 bytes of O; NT: a non-temporal (streaming) store.  Only for whole-row stores (the O row
-// image): O is written once, and the final drain of every CU at once is the mirrored kernel's
-// tail (C2 +2.4-2.8 %).  Row-per-lane stores (16-32 B per row and instruction) lose with NT
-// (C3 -4.9 %, C5 forward -11.5 %): their partial lines are no longer merged in L2.
-template <bool NT>
-__device__ __forceinline__ void st_o4(float* dst, float a, float b, float c, float d) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  if constexpr (NT)
-    __builtin_nontemporal_store(f4v{a, b, c, d}, reinterpret_cast<f4v*>(dst));
-  else
-    *reinterpret_cast<f4v*>(dst) = f4v{a, b, c, d};
-}
-
-template <int DP, bool NT = false>
-__device__ __forceinline__ void store_o_l(const FwdParams& p, const f32x16 (&o)[DP / 32],
-                                          float m, float l, int b, int h, int qi, int hh) {
-  const float inv = p.o_mul / l;
-  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)qi * p.o_ss;
-#pragma unroll
-  for (int dt = 0; dt < DP / 32; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = dt * 32 + 8 * g + 4 * hh;
-      if (d < p.D)
-        st_o4<NT>(orow + d, o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
-                  o[dt][4 * g + 3] * inv);
-    }
-  if (hh == 0) {
-    const float L = m + __log2f(l);
-    const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
-    if (p.l_f16)
-      reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
-    else
-      reinterpret_cast<float*>(p.l)[li] = L;
-  }
-}
-
-__device__ __forceinline__ void key_range(const FwdParams& p, int q0, int BQ, int BK, int* kbeg,
-                                          int* kend) {
-  *kend = p.C;
-  if (p.mask.causal) *kend = min(*kend, q0 + BQ);
-  *kbeg = 0;
-  if (p.mask.window) {
-    const int64_t lo = (int64_t)q0 - (int64_t)p.mask.window_size;
-    *kbeg = lo > 0 ? (int)(lo / BK) * BK : 0;
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // One 128-row query block per workgroup (4 waves x 32 rows); WPS workgroups' waves per SIMD.
@@ -372,6 +62,53 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
 
   int kbeg, kend;
   key_range(p, q0, BQ, BK, &kbeg, &kend);
+  // Sparse ranges (SparseMQABuilder, AttentionKernel+Softmax.swift:278-304): the row's keys
+  // [x, y); tiles outside the union of the block's non-empty ranges are skipped.  Rows left
+  // with no unmasked key are rewritten by mfa_fwd_masked_rows_kernel (the reference's finite
+  // mask value makes them a uniform average over every key).
+  int rlo = -0x40000000, rhi = 0x3fffffff;
+  int in_lo = 0, in_hi = 0x3fffffff;  // keys inside every non-empty range of the block
+  if (p.mask.ranges) {
+    uint32_t x = 0u, y = 0u;
+    if (qvalid) {
+      const uint32_t* rp = p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + qi);
+      x = rp[0];
+      y = rp[1];
+    }
+    rlo = (int)min(x, 0x3fffffffu);
+    rhi = (int)min(y, 0x3fffffffu) - 1;
+    // Empty rows are rewritten afterwards, so they constrain neither the union nor the
+    // range-free interior.
+    const bool ne = x < y;
+    int mn = ne ? rlo : 0x3fffffff, mx = ne ? rhi + 1 : 0;
+    in_lo = ne ? rlo : 0;
+    in_hi = ne ? rhi + 1 : 0x3fffffff;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mn = min(mn, __shfl_xor(mn, o));
+      mx = max(mx, __shfl_xor(mx, o));
+      in_lo = max(in_lo, __shfl_xor(in_lo, o));
+      in_hi = min(in_hi, __shfl_xor(in_hi, o));
+    }
+    int* red = reinterpret_cast<int*>(smem);
+    if (lane == 0) {
+      red[4 * wave] = mn;
+      red[4 * wave + 1] = mx;
+      red[4 * wave + 2] = in_lo;
+      red[4 * wave + 3] = in_hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      mn = min(mn, red[4 * w]);
+      mx = max(mx, red[4 * w + 1]);
+      in_lo = max(in_lo, red[4 * w + 2]);
+      in_hi = min(in_hi, red[4 * w + 3]);
+    }
+    __syncthreads();  // the reduction slots are the first K slot's bytes
+    kbeg = max(kbeg, (mn / BK) * BK);
+    kend = min(kend, mx);
+  }
   DmaA<DP, BK, NT> kd, vd;
   kd.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
   vd.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
@@ -410,9 +147,10 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
         }
       }
     };
-    const bool mask_tile = (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
+    const bool mask_tile = (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) ||
+                           p.mask.window || t < in_lo || t + BK > in_hi;
     fwd2_tile<E, DP, BK, TU>(kb0 + cur * TILEB, vb0 + cur * TILEB, rbase, trb, qf, st, t, mask_tile,
-                         qi, p, c, wsz, hh, hook);
+                         qi, p, c, wsz, hh, hook, rlo, rhi);
     MFA_ACC(1);
     wait_vm();
     __syncthreads();
@@ -1022,6 +760,65 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
   return launch(kern, dim3(npairs * p.B * p.H), dim3(NWG * 128), LDS, stream, q);
 }
 
+// ---------------------------------------------------------------------------------------
+// Rows with no unmasked key (empty sparse range, or a range the causal / window predicates
+// empty).  The reference masks with a finite value (AttentionKernel+Softmax.swift:257), so
+// such a row sees the same score for every key: P = 1, O = Σ_k V_k / C, and L = m + log2 C
+// with m = (mask value)·c as the forward computes it.  One thread tests each query row; a
+// wave then rewrites its empty rows together.  Runs after the tuned forward, which masks
+// with -inf.
+template <class E>
+__global__ void __launch_bounds__(256) mfa_fwd_masked_rows_kernel(FwdParams p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nrows = (int64_t)p.B * p.H * p.R;
+  const int64_t rid = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (b·H + h)·R + q
+  bool empty = false;
+  if (rid < nrows) {
+    const int q = (int)(rid % p.R);
+    const int bh = (int)(rid / p.R);
+    const int h = bh % p.H, b = bh / p.H, kvh = h % p.Hkv;
+    const uint32_t* rp = p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + q);
+    int64_t lo = rp[0], hi = min((int64_t)rp[1], (int64_t)p.C);
+    if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
+    if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
+    empty = lo >= hi;
+  }
+  // The wave walks its empty rows together, lanes across the head dimension.
+  uint64_t todo = __ballot(empty);
+  while (todo) {
+    const int src = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int64_t r = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63) + src;
+    const int q = (int)(r % p.R);
+    const int bh = (int)(r / p.R);
+    const int h = bh % p.H, b = bh / p.H, kvh = h % p.Hkv;
+    const uint16_t* vbase = (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
+    float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
+    const float l = (float)p.C;
+    for (int d = lane; d < p.D; d += 64) {
+      float acc = 0.f;
+      for (int k = 0; k < p.C; ++k) acc += E::to_f32(vbase[(int64_t)k * p.v.ss + (int64_t)d * p.v.sd]);
+      orow[(int64_t)d * p.o_sd] = acc * (p.o_mul / l);
+    }
+    if (lane == 0) {
+      const float L = mul_rn(kMaskValue, p.c_log2) + __log2f(l);
+      const int64_t li = (int64_t)(b * p.H + h) * p.R + q;
+      if (p.l_f16)
+        reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+      else
+        reinterpret_cast<float*>(p.l)[li] = L;
+    }
+  }
+}
+
+hipError_t fwd_masked_rows_dispatch(const FwdParams& p, int elem, hipStream_t stream) {
+  const int64_t rows = (int64_t)p.B * p.H * p.R;
+  const dim3 grid((unsigned)((rows + 255) / 256));
+  if (elem == P_FP16) return launch(mfa_fwd_masked_rows_kernel<F16>, grid, dim3(256), 0, stream, p);
+  if (elem == P_BF16) return launch(mfa_fwd_masked_rows_kernel<BF16>, grid, dim3(256), 0, stream, p);
+  return hipErrorNotSupported;
+}
+
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   const char* var = getenv("MFA_FWD_VARIANT");
@@ -1029,7 +826,8 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   // Causal: mirrored pairs while they fill at most ~1.5 rounds of the chip, or up to 3 rounds
   // for long rows (S >= 8192: 64 blocks; one-process A/B: H16 S8192 1057 vs 987 TF single,
   // B2 H16 S8192 1027 vs 1043, B2 H16 S4096 881 vs 889).
-  bool single = !p.mask.causal || DP > 128 || (blocks > 768 && !(p.nblk >= 64 && blocks <= 1536));
+  bool single = !p.mask.causal || DP > 128 || (blocks > 768 && !(p.nblk >= 64 && blocks <= 1536)) ||
+                p.mask.ranges;
   if (var && var[0] == 's') single = true;
   if (var && var[0] == 'p') single = false;
   // Development A/B of the scheduling knobs on the fp16 D=128 single-block kernel.
@@ -1058,7 +856,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   // any size (tests).
   const char* sv = getenv("MFA_FWD_SHARE");
   // (An odd block count leaves group 1 of the last pair without rows: not for nblk < 8 odd.)
-  const bool adj = !p.mask.causal && !p.mask.window && !var &&
+  const bool adj = !p.mask.causal && !p.mask.window && !p.mask.ranges && !var &&
                    (sv ? sv[0] == '1'
                        : (p.nblk % 2 == 0 || p.nblk >= 8) &&
                              (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);

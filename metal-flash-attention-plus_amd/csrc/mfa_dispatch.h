@@ -67,6 +67,9 @@ hipError_t bwd_bigd_dispatch(const BwdParams& p, int kind, int elem, hipStream_t
 // needs (partials of every wave).
 size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D);
 hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hipStream_t stream);
+// Rows with no unmasked key after a sparse-range forward on the tuned kernel: O = mean of V,
+// L as the reference's finite mask value gives it (attention_fwd_v2.hip).
+hipError_t fwd_masked_rows_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Dense 16-bit copy [B, Hx, S, D] of a quantised operand holding the MFMA operands the

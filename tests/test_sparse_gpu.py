@@ -1,0 +1,104 @@
+"""GPU parity for sparse key ranges on the tuned 16-bit forward (attention_fwd_v2.hip).
+
+The HAS_SPARSE_RANGES mask (AttentionKernel+Softmax.swift:278-304) gives every query row a
+half-open key range [x, y), indexed (b*H_kv + kv)*R + row; SparseMQABuilder.buildBlockSparse
+(SparseMQABuilder.swift:30-62) turns a block pattern into such ranges.  The tuned kernel skips
+the key tiles outside the union of a query block's ranges; rows left with no unmasked key get
+the reference's finite-mask result (uniform average of V, L = mask*c + log2 C) from a fix-up
+pass.  Tolerances: SquareAttentionTest.swift:557-571 (mixed O 5e-2); L here is kept in fp32
+(lowPrecisionIntermediates off) so the fully masked rows' L stays finite.
+"""
+import numpy as np
+import pytest
+import torch
+
+import mfa_amd as mfa
+import oracle_lib as ol
+from harness import maxerr, run_forward, seen
+
+pytestmark = pytest.mark.gpu
+FP16, BF16 = mfa.Precision.FP16, mfa.Precision.BF16
+
+
+def gaussian(shape, seed):
+    return np.random.default_rng(seed).standard_normal(shape).astype(np.float32)
+
+
+def block_ranges(pattern, block, R, C):
+    """Per-row ranges from a [R/block, C/block] pattern through the library's builder."""
+    nqb, nkb = pattern.shape
+    rb = np.zeros((nqb, 2), dtype=np.uint32)
+    mfa.lib.mfa_sparse_build_block_sparse(np.ascontiguousarray(pattern, dtype=np.uint8).ctypes.data,
+                                          nqb, nkb, block, rb.ctypes.data)
+    rows = np.repeat(rb, block, axis=0)[:R]
+    rows[:, 1] = np.minimum(rows[:, 1], C)
+    return rows
+
+
+def banded_pattern(nqb, nkb, width, seed, empty_every=0):
+    rng = np.random.default_rng(seed)
+    pat = np.zeros((nqb, nkb), dtype=np.uint8)
+    for i in range(nqb):
+        c = min(nkb - 1, i * nkb // nqb + int(rng.integers(-1, 2)))
+        pat[i, max(0, c - width // 2):min(nkb, c + width // 2 + 1)] = 1
+        if empty_every and i % empty_every == empty_every - 1:
+            pat[i] = 0
+    return pat
+
+
+def check(Q, K, V, prec, ranges, causal=False, window=None):
+    o, l = run_forward(Q, K, V, prec=prec, causal=causal, window=window, ranges=ranges,
+                       low_precision_intermediates=False)
+    plan = [x["name"] for x in mfa.last_launches()]
+    ref = ol.attention(seen(Q, prec), seen(K, prec), seen(V, prec), causal=causal, window=window,
+                       ranges=ranges)
+    on, ln = o.cpu().numpy(), l.float().cpu().numpy()
+    assert np.isfinite(on).all()
+    assert maxerr(on, ref["O"]) <= 5e-2
+    # Rows with a key keep L ~ O(10); fully masked rows carry L = fp32(mask * c) + log2 C.
+    big = np.abs(ref["L"]) > 1e6
+    assert maxerr(ln[~big], ref["L"][~big]) <= 1e-2
+    if big.any():
+        assert np.allclose(ln[big], ref["L"][big], rtol=1e-6, atol=0)
+    return plan
+
+
+@pytest.mark.parametrize("prec", [FP16, BF16])
+@pytest.mark.parametrize("D", [64, 128])
+def test_block_sparse_tuned_kernel(gpu, prec, D):
+    B, H, Hkv, S, blk = 1, 4, 2, 1000, 64
+    nb = (S + blk - 1) // blk
+    ranges = np.stack([block_ranges(banded_pattern(nb, nb, 3, 900 + kv), blk, S, S)
+                       for kv in range(Hkv)])[None]
+    Q = gaussian((B, H, S, D), 901)
+    K, V = gaussian((B, Hkv, S, D), 902), gaussian((B, Hkv, S, D), 903)
+    plan = check(Q, K, V, prec, ranges)
+    assert any("mfa_fwd2_kernel" in n for n in plan), plan
+    assert any("masked_rows" in n for n in plan), plan
+
+
+@pytest.mark.parametrize("causal,window", [(True, None), (False, 90), (False, 300)])
+def test_block_sparse_with_empty_rows_and_masks(gpu, causal, window):
+    """Empty block rows, and rows whose range the causal / window predicates empty, take the
+    finite-mask uniform average; the union skip must not drop keys other rows need."""
+    B, H, Hkv, R, C, D, blk = 2, 2, 1, 700, 700, 128, 64
+    nb = (R + blk - 1) // blk
+    ranges = np.stack([block_ranges(banded_pattern(nb, nb, 5, 910 + b, empty_every=4), blk, R, C)
+                       for b in range(B)])[:, None]
+    # Ragged per-row ranges inside a block: some rows empty, some narrowed.
+    ranges[0, 0, 5::11, 1] = ranges[0, 0, 5::11, 0]
+    ranges[1, 0, 3::13, 0] = np.minimum(ranges[1, 0, 3::13, 0] + 17, ranges[1, 0, 3::13, 1])
+    Q = gaussian((B, H, R, D), 911)
+    K, V = gaussian((B, Hkv, C, D), 912), gaussian((B, Hkv, C, D), 913)
+    check(Q, K, V, FP16, ranges, causal=causal, window=window)
+
+
+def test_ranges_beyond_sequence(gpu):
+    """Ranges reaching past C (the reference clamps at the key bound) and x >= y rows."""
+    B, H, R, C, D = 1, 2, 300, 257, 64
+    lo = np.random.default_rng(920).integers(0, C + 40, (B, H, R))
+    hi = lo + np.random.default_rng(921).integers(-5, 200, (B, H, R))
+    ranges = np.stack([lo, np.maximum(hi, 0)], -1).astype(np.uint32)
+    Q = gaussian((B, H, R, D), 922)
+    K, V = gaussian((B, H, C, D), 923), gaussian((B, H, C, D), 924)
+    check(Q, K, V, BF16, ranges)
