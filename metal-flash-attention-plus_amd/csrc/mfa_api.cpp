@@ -697,6 +697,29 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
   return (int64_t)p.C * p.k.ss < ((int64_t)1 << 31);
 }
 
+// The on-load shared-tile forward (attention_fwd_kv8.hip): FP16 Q, per-tensor INT8 or INT4
+// K/V (any zero point), D % 16 == 0 with D <= 128 padded to 128, no masks, dense rows with
+// 16-byte aligned byte offsets.  MFA_KV8=0 routes these through the dequantisation pass
+// instead (A/B).
+bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int DP) {
+  if (const char* e = getenv("MFA_KV8")) {
+    if (e[0] == '0') return false;
+  }
+  if (elem != 1 || qp != MFA_PRECISION_FP16) return false;
+  if (kp != vp || (kp != MFA_PRECISION_INT8 && kp != MFA_PRECISION_INT4)) return false;
+  if (p.k.bscale || p.v.bscale) return false;
+  if (DP != 128 || p.D % 16 != 0 || !(p.c_log2 > 0.f)) return false;
+  const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
+  if (p.mask.causal || p.mask.window || p.mask.amask || p.mask.ranges) return false;
+  if (p.q.sd != 1 || !p.q.vec || p.o_sd != 1) return false;
+  if (p.k.sd != 1 || p.v.sd != 1) return false;
+  for (const mfa::Operand* o : {&p.k, &p.v})
+    if (o->ss % (16 << sh) || o->sh % (16 << sh) || o->sb % (16 << sh) ||
+        (uintptr_t)o->ptr % 16)
+      return false;
+  return (int64_t)p.C * p.k.ss < ((int64_t)1 << 31) && (int64_t)p.C * p.v.ss < ((int64_t)1 << 31);
+}
+
 // Quantised operands go through one dequantisation pass into a dense 16-bit copy
 // (kv_dequant.hip) when the compute type is 16-bit, D % 8 == 0 and each kv head serves at
 // least 128 query rows: every element is then converted once per call instead of once per
@@ -814,6 +837,9 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     const hipError_t e = mfa::fwd_decode_dispatch(p, elem, ws, (hipStream_t)stream);
     if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (decode) launch");
   }
+  if (kv8_eligible(p, elem, qp, kp, vp, DP))
+    return hip_status(mfa::fwd_kv8_dispatch(p, elem, src_kind(kp), (hipStream_t)stream),
+                      "mfa_fwd (INT8 K/V on load) launch");
   int kvsrc = src_kind(kp);
   if (dequant_pass_worth(R, H, Hkv, D, elem)) {
     hipStream_t s = (hipStream_t)stream;

@@ -87,28 +87,41 @@ def test_quantized_plans():
     base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
     qi = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, integer_matmul=True)
     assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 128, 2, 2>"
-    # Dequant-exact: one dequantisation pass per quantised operand (kv_dequant.hip), then the
-    # tuned 16-bit kernel on the dense copies.
+    # Dequant-exact forward, FP16 Q + per-tensor INT8 K/V: one kernel widening the bytes as
+    # it stages them (attention_fwd_kv8.hip), no pass.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
-    names = [r["name"] for r in mfa.quantized_plan(qx)]
-    assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
-    assert names[2] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>" and len(names) == 3
+    assert [r["name"] for r in mfa.quantized_plan(qx)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, 1, 3, 12, 14>"]
+    # The backward: one dequantisation pass per quantised operand (kv_dequant.hip), then the
+    # tuned 16-bit kernel on the dense copies.
     for kind, kern in ((K.backwardQuery, "mfa_bwd_q_fast_kernel<F16, 128, 64>"),
                        (K.backwardKeyValue, "mfa_bwd_kv_fast_kernel<F16, 128, 64>")):
         assert [r["name"] for r in mfa.quantized_plan(qx, kind)][2] == kern
-    # INT4 and a quantised Q take the same pass (SRC_I4 = 2).
+    # INT4 K/V with an FP16 Q: the same on-load kernel (SRC_I4 = 2).
+    q4h = mfa.quantized_descriptor(base, P.FP16, P.INT4, P.INT4, B=1, H=16)
+    assert [r["name"] for r in mfa.quantized_plan(q4h)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2, 1, 3, 12, 14>"]
+    # A quantised Q takes the dequantisation pass for every operand.
     q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(q4)]
     assert names[:3] == ["mfa_kv_dequant_kernel<F16, 2>"] * 2 + ["mfa_kv_dequant_kernel<F16, 1>"]
     assert names[3] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>"
     # A non-zero zero point leaves the integer-matmul kernel (dequant-exact path instead).
     zp = mfa.QuantizedTensor(None, int(P.INT8), 0.5, 3)
-    assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_share_kernel<")
+    assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_kv8_kernel<")
     # Decode-like shapes (few query rows per kv head) read the quantised tensors directly.
     dec = mfa.AttentionDescriptor.make(16, 8192, 128, low_precision=True, precision=P.FP16)
     qd = mfa.quantized_descriptor(dec, P.FP16, P.INT8, P.INT8, B=1, H=4)
     names = [r["name"] for r in mfa.quantized_plan(qd)]
     assert names == ["mfa_fwd_decode_kernel<F16, 128>", "mfa_decode_merge_kernel"], names
+
+
+def test_kv8_override_takes_the_dequant_pass(monkeypatch):
+    # MFA_KV8=0 (A/B): the dequantisation pass + the 16-bit shared-tile kernel instead.
+    monkeypatch.setenv("MFA_KV8", "0")
+    base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
+    qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
+    names = [r["name"] for r in mfa.quantized_plan(qx)]
+    assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
+    assert names[2] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>" and len(names) == 3
 
 
 def test_environment_override_is_visible_in_plan(monkeypatch):

@@ -532,3 +532,64 @@ def test_decode_nonzero_zero_point(gpu):
     Vd = (vq.astype(np.float32) - vz) * np.float32(vs)
     ref = ol.attention(seen(Q, P.FP16), Kd, Vd)
     assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
+
+
+# FP16 Q with per-tensor INT8 K/V at >= 128 query rows per kv head: the shared-tile kernel
+# widens the staged bytes to the integers q - zp inside its loop (attention_fwd_kv8.hip), with
+# the scales folded as in the dequantisation pass.  Held to the oracle on the dequantised
+# values and to the pass + 16-bit kernel path (MFA_KV8=0): bit-identical at D = 128, where the
+# two run the same tile loop on the same operands.
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,zps", [
+    (1, 4, 4, 300, 1000, 128, (0, 0)),    # odd block count: the last pair's group 1 idles
+    (2, 4, 2, 256, 333, 128, (0, 0)),     # GQA, partial last key tile
+    (1, 2, 2, 129, 4101, 96, (7, -5)),    # zero points, ragged rows and keys
+    (1, 8, 1, 512, 200, 112, (0, 3)),     # MQA
+])
+def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, monkeypatch):
+    rng = np.random.default_rng(R + C + D)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    lim = 120 if kv == P.INT8 else 8
+    kq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    vq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    ks, vs = 0.015, 0.02
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=P.FP16)
+    desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    if kv == P.INT8:
+        kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
+    else:  # nibble n encodes n - 8, element 2i in the low nibble (GEMMQuantization.swift:500-515)
+        pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
+        kt, vt = tdev(pack(kq.astype(np.int32)), torch.uint8), tdev(pack(vq.astype(np.int32)), torch.uint8)
+    tk = mfa.quantized_tensor(kt, kv, scale=ks, zero_point=zps[0])
+    tv = mfa.quantized_tensor(vt, kv, scale=vs, zero_point=zps[1])
+    src = 1 if kv == P.INT8 else 2
+    names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    if kv == P.INT8 or D % 32 == 0:
+        assert names == [f"mfa_fwd2_kv8_kernel<F16, 128, 64, {src}, 1, 3, 12, 14>"], names
+    else:  # INT4 rows of D / 2 bytes off 16-byte alignment: the dequantisation pass
+        assert names[0] == "mfa_kv_dequant_kernel<F16, 2>", names
+
+    def run():
+        o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
+        l = torch.full((B, H, R), float("nan"), dtype=torch.float16, device=DEV)
+        mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+        torch.cuda.synchronize()
+        return o.cpu().numpy(), l.float().cpu().numpy()
+
+    o1, l1 = run()
+    monkeypatch.setenv("MFA_KV8", "0")
+    o2, l2 = run()
+    monkeypatch.delenv("MFA_KV8")
+    kd = ((kq.astype(np.float32) - zps[0]) * np.float32(ks)).astype(np.float32)
+    vd = ((vq.astype(np.float32) - zps[1]) * np.float32(vs)).astype(np.float32)
+    Qs = seen(Q, P.FP16)
+    for h in sorted({0, H - 1}):
+        ref = ol.attention(Qs[:, h:h + 1], kd[:, h % Hkv:h % Hkv + 1], vd[:, h % Hkv:h % Hkv + 1])
+        assert maxerr(o1[:, h:h + 1], ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max()), h
+        assert maxerr(l1[:, h:h + 1], ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max(), h
+    assert np.isfinite(o1).all()
+    if D == 128:
+        assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
+    else:
+        assert maxerr(o1, o2) < 1e-5 and maxerr(l1, l2) < 2e-2

@@ -1,0 +1,87 @@
+"""One-process A/B of library environment knobs on a bench workload (development tool).
+
+Usage: python tools/ab_env.py WORKLOAD VAR=a,b,c [VAR2=x,y] — times each setting by HIP
+events (median of 5 rounds of 20 launches), interleaving settings round by round.
+WORKLOAD: c3_int8_exact | c3_fp16 | c2
+"""
+import itertools
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "metal-flash-attention-plus_amd", "python"))
+import mfa_amd as mfa  # noqa: E402
+
+
+def workload(name, dev="cuda:0"):
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    u = lambda shape, dt: ((torch.rand(shape, generator=g, device=dev) * 2 - 1) * 0.25).to(dt)
+    stream = torch.cuda.current_stream().cuda_stream
+    if name.startswith("c3"):
+        B, H, S, D = 1, 16, 8192, 128
+        q = u((B, H, S, D), torch.float16)
+        kf, vf = u((B, H, S, D), torch.float32), u((B, H, S, D), torch.float32)
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+        base = mfa.AttentionDescriptor.make(S, S, D, low_precision=True, precision=mfa.Precision.FP16)
+        flops = mfa.attention_flops(B, H, S, S, D)
+        if name == "c3_fp16":
+            desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+            kh, vh = kf.half(), vf.half()
+            return (lambda: mfa.MultiHeadAttention().forward(desc, q, kh, vh, o, l, stream=stream)), flops
+        kq, ks, _, _ = mfa.quantize(kf, mfa.Precision.INT8, rows=B * H * S, cols=D)
+        vq, vs, _, _ = mfa.quantize(vf, mfa.Precision.INT8, rows=B * H * S, cols=D)
+        qd = mfa.quantized_descriptor(base, mfa.Precision.FP16, mfa.Precision.INT8, mfa.Precision.INT8, B=B, H=H)
+        tq = mfa.quantized_tensor(q, mfa.Precision.FP16)
+        tk = mfa.quantized_tensor(kq, mfa.Precision.INT8, scale=float(ks.item()))
+        tv = mfa.quantized_tensor(vq, mfa.Precision.INT8, scale=float(vs.item()))
+        qa = mfa.QuantizedAttention()
+        return (lambda: qa.forward(qd, tq, tk, tv, o, l, stream=stream)), flops
+    if name == "c2":
+        B, H, S, D = 1, 16, 4096, 128
+        q, k, v = (u((B, H, S, D), torch.float16) for _ in range(3))
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16, causal=True)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+        return (lambda: mfa.MultiHeadAttention().forward(desc, q, k, v, o, l, stream=stream)), \
+            mfa.attention_flops(B, H, S, S, D, causal=True)
+    raise SystemExit(f"unknown workload {name}")
+
+
+def main():
+    name = sys.argv[1]
+    axes = []
+    for a in sys.argv[2:]:
+        k, vals = a.split("=", 1)
+        axes.append([(k, v) for v in vals.split(",")])
+    settings = list(itertools.product(*axes)) or [()]
+    fn, flops = workload(name)
+    times = {s: [] for s in settings}
+    for _ in range(60):
+        fn()
+    torch.cuda.synchronize()
+    for _ in range(5):
+        for s in settings:
+            for k, v in s:
+                os.environ[k] = v
+            for _ in range(5):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                fn()
+            e1.record()
+            e1.synchronize()
+            times[s].append(e0.elapsed_time(e1) / 20)
+    for s in settings:
+        ms = statistics.median(times[s])
+        print(f"{name} {' '.join(f'{k}={v}' for k, v in s) or '(default)'}: {ms * 1e3:.1f} us "
+              f"{flops / ms / 1e9:.1f} TFLOPS", flush=True)
+
+
+if __name__ == "__main__":
+    main()
