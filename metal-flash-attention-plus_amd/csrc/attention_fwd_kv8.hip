@@ -6,12 +6,13 @@
 // mfa_fwd2_share_kernel with MIRROR = false): 512 threads own query blocks 2·pi and 2·pi + 1
 // (one 4-wave group each) and every K/V tile feeds both, 256 query rows per staged tile.
 // Per step s, each thread:
-//   - loads its 16-byte chunk of tile s + 2's K and V bytes into registers (global loads, one
-//     step of latency cover; no LDS staging, so LDS traffic equals the 16-bit kernel's);
-//   - widens the chunk of tile s + 1 loaded one step earlier to the exact integers q − zp in
-//     FP16 (magic-number v_perm + packed subtract, mfa_stage.h dequant_fast) and writes it into
-//     the 16-bit TileA image slot of tile s + 1, in four pieces placed between the MFMAs of
-//     tile s's QKᵀ and PV chains;
+//   - widens its 16-byte chunk of tile s + 1's K and V bytes (in registers since step s − 1)
+//     to the exact integers q − zp in FP16 (magic-number v_perm + packed subtract,
+//     mfa_stage.h dequant_fast) and writes it into the 16-bit TileA image slots of tile s + 1,
+//     in four pieces placed between the MFMAs of tile s's QKᵀ and PV chains;
+//   - right after each widening, loads the same chunk of tile s + 2 into the freed registers
+//     (global loads, about one step of latency cover; no LDS staging, so the LDS traffic is
+//     the 16-bit kernel's);
 //   - runs tile s from its 16-bit image exactly as the 16-bit kernel does.
 // Per-tensor scales stay folded in the softmax multiplier (K) and the output multiplier (V),
 // so the MFMA operands, and hence O and L, are bit-identical to the dequantise pass +
@@ -84,50 +85,46 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   const int vbytes = (int)((int64_t)(p.C - 1) * vss + (p.D >> SH));
   const int kro = cvalid ? cr * kss + cc * CB : 0x40000000;
   const int vro = cvalid ? cr * vss + cc * CB : 0x40000000;
-  // This thread's chunk of tile t's K and V bytes.
-  auto load8 = [&](int t, uint4& rk, uint4& rv) {
-    const int kb = t * kss, vb = t * vss;
-    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(khead + kb), (short)0, max(kbytes - kb, 0), 0x00020000);
-    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(vhead + vb), (short)0, max(vbytes - vb, 0), 0x00020000);
+  // This thread's chunk of tile t's K (V) bytes.
+  auto load1 = [&](const char* head, int ss, int bytes, int ro, int t) -> uint4 {
+    const int tb = t * ss;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(head + tb), (short)0, max(bytes - tb, 0), 0x00020000);
     if constexpr (SRC == SRC_I8) {
-      const auto a = __builtin_amdgcn_raw_buffer_load_b128(krs, kro, 0, 0);
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(vrs, vro, 0, 0);
-      rk = make_uint4(a[0], a[1], a[2], a[3]);
-      rv = make_uint4(v[0], v[1], v[2], v[3]);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, ro, 0, 0);
+      return make_uint4(a[0], a[1], a[2], a[3]);
     } else {
-      const auto a = __builtin_amdgcn_raw_buffer_load_b64(krs, kro, 0, 0);
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(vrs, vro, 0, 0);
-      rk = make_uint4(a[0], a[1], 0u, 0u);
-      rv = make_uint4(v[0], v[1], 0u, 0u);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b64(rs, ro, 0, 0);
+      return make_uint4(a[0], a[1], 0u, 0u);
     }
   };
+  auto loadk = [&](int t) { return load1(khead, kss, kbytes, kro, t); };
+  auto loadv = [&](int t) { return load1(vhead, vss, vbytes, vro, t); };
 
   const int q0 = (2 * pi + g) * BQ;
   const int qi = q0 + wg * 32 + l32;
   i16x8 qf[DP / 16];
-  uint4 ka, va, kb, vb;
-  load8(0, ka, va);
-  load8(BK, kb, vb);
+  // rk / rv: the bytes of the next tile to widen.  Each is reloaded (tile s + 2) as soon as
+  // its widening into tile s + 1's slot has been issued, one step ahead of its use.
+  uint4 rk = loadk(0), rv = loadv(0);
   load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
   prescale_q2<E, DP>(qf, c);
-  widen_store<E, DP, SRC, 0>(sk, cr, cc, ka, zk);
-  widen_store<E, DP, SRC, 1>(sk, cr, cc, ka, zk);
-  widen_store<E, DP, SRC, 0>(sv, cr, cc, va, zv);
-  widen_store<E, DP, SRC, 1>(sv, cr, cc, va, zv);
+  widen_store<E, DP, SRC, 0>(sk, cr, cc, rk, zk);
+  widen_store<E, DP, SRC, 1>(sk, cr, cc, rk, zk);
+  widen_store<E, DP, SRC, 0>(sv, cr, cc, rv, zv);
+  widen_store<E, DP, SRC, 1>(sv, cr, cc, rv, zv);
+  rk = loadk(BK);
+  rv = loadv(BK);
   __syncthreads();
 
   RowState<DP> st;
   st.init();
   const int wsz = 0x3fffffff;
-  // Step s: the registers `w` hold tile s + 1's bytes (loaded one step ago) and are widened
-  // into the 16-bit slot of tile s + 1 between the MFMAs; `ld` takes tile s + 2's bytes.
-  // On the last steps the widening writes stale bytes into the slot of a tile already
-  // consumed: harmless, and the MFMA chains stay branch-free.
-  auto step = [&](int s, uint4& wk, uint4& wv, uint4& lk, uint4& lv) {
+  // Step s widens tile s + 1 into its 16-bit slots between the MFMAs of tile s.  On the last
+  // steps the widening writes stale bytes into the slot of a tile already consumed: harmless,
+  // and the MFMA chains stay branch-free.
+  for (int s = 0; s < n; ++s) {
     const int cur = s & 1, nx = cur ^ 1;
-    load8((s + 2) * BK, lk, lv);
     const int t = s * BK;
     const bool mask_tile = t + BK > p.C;
     f32x16 sc[BK / 32];
@@ -135,23 +132,25 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
     char* const knext = sk + nx * TILEB;
     char* const vnext = sv + nx * TILEB;
     // The widening in four pieces (5 VALU + one 16-byte LDS write each), one per MFMA gap.
-    fwd2_qk<E, DP, BK>(sk + cur * TILEB, rbase, qf, st, sc, [&](int i) {
-      if (i == KP0) widen_store<E, DP, SRC, 0>(knext, cr, cc, wk, zk);
-      if (i == KP1) widen_store<E, DP, SRC, 1>(knext, cr, cc, wk, zk);
-    });
+    auto khook = [&](int i) {
+      if (i == KP0) widen_store<E, DP, SRC, 0>(knext, cr, cc, rk, zk);
+      if (i == KP1) {
+        widen_store<E, DP, SRC, 1>(knext, cr, cc, rk, zk);
+        rk = loadk(t + 2 * BK);
+      }
+    };
+    auto vhook = [&](int i) {
+      if (i == VP0) widen_store<E, DP, SRC, 0>(vnext, cr, cc, rv, zv);
+      if (i == VP1) {
+        widen_store<E, DP, SRC, 1>(vnext, cr, cc, rv, zv);
+        rv = loadv(t + 2 * BK);
+      }
+    };
+    fwd2_qk<E, DP, BK>(sk + cur * TILEB, rbase, qf, st, sc, khook);
     fwd2_softmax<E, DP, BK>(st, sc, pb, t, mask_tile, qi, p, c, wsz, hh);
-    fwd2_pv<E, DP, BK>(sv + cur * TILEB, trb, pb, st, [&](int i) {
-      if (i == VP0) widen_store<E, DP, SRC, 0>(vnext, cr, cc, wv, zv);
-      if (i == VP1) widen_store<E, DP, SRC, 1>(vnext, cr, cc, wv, zv);
-    });
+    fwd2_pv<E, DP, BK>(sv + cur * TILEB, trb, pb, st, vhook);
     __syncthreads();
-  };
-  int s = 0;
-  for (; s + 1 < n; s += 2) {
-    step(s, kb, vb, ka, va);
-    step(s + 1, ka, va, kb, vb);
   }
-  if (s < n) step(s, kb, vb, ka, va);
 
   // Both blocks leave through O row images (one per group) as whole rows from all 8 waves.
   float l = cross_half_sum(st.lh) + kFltMin;
