@@ -86,9 +86,9 @@ def test_int8_launches_match_plan(gpu, integer_matmul):
     assert mfa.last_launches() == plan
     if integer_matmul:
         assert len(plan) == 1 and plan[0]["name"].startswith("mfa_fwd_i8_kernel<")
-    else:  # dequantisation pass for K and V, then the tuned 16-bit forward
-        assert [r["name"] for r in plan[:2]] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
-        assert len(plan) == 3 and plan[2]["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>"
+    else:  # K/V bytes dequantised on load inside the shared-tile forward: one launch, no pass
+        assert len(plan) == 1 and plan[0]["name"].startswith("mfa_fwd2_kv8_kernel<F16, 128, 64,")
+        assert not any(r["name"].startswith("mfa_kv_dequant_kernel") for r in plan)
 
 
 @pytest.mark.parametrize("D,causal", [(128, True), (256, False)])
