@@ -822,12 +822,6 @@ hipError_t fwd_masked_rows_dispatch(const FwdParams& p, int elem, hipStream_t st
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   const char* var = getenv("MFA_FWD_VARIANT");
-  if (const char* pp = getenv("MFA_FWD_PP")) {
-    if (pp[0] == '1') {
-      const hipError_t e = fwd_pp_dispatch(p, elem, DP, stream);
-      if (e != hipErrorNotSupported) return e;
-    }
-  }
   const int blocks = p.nblk * p.B * p.H;
   // Causal: mirrored pairs while they fill at most ~1.5 rounds of the chip, or up to 3 rounds
   // for long rows (S >= 8192: 64 blocks; one-process A/B: H16 S8192 1057 vs 987 TF single,
