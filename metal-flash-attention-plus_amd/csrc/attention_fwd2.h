@@ -306,6 +306,37 @@ __device__ __forceinline__ void st_o4(float* dst, float a, float b, float c, flo
     *reinterpret_cast<f4v*>(dst) = f4v{a, b, c, d};
 }
 
+// Rows [q0, q0 + NR) of an O row image (rows of DP floats at a pitch of ORS bytes) leave as
+// 16-byte chunks from all NTH threads, thread t taking chunk t % CPR of rows t / CPR + k·NTH/CPR.
+// Every image read is issued before the first store and, for a full block (all rows below R,
+// D = DP), the stores are unguarded with the row address advanced by a constant: the guarded
+// per-store form compiles to one read -> wait -> store round trip per chunk (~300 cycles each
+// at the mirrored kernel's switch).
+template <int DP, int NR, int NTH, bool NT>
+__device__ __forceinline__ void store_o_image(const FwdParams& p, float* obase, const char* img,
+                                              int ors, int q0, int tid, bool full) {
+  constexpr int CPR = DP / 4, OST = NR * CPR / NTH, RPK = NTH / CPR;
+  static_assert(NTH % CPR == 0 && NR * CPR % NTH == 0, "O image store geometry");
+  const int r0 = tid / CPR, d = (tid % CPR) * 4;
+  float4 v[OST];
+#pragma unroll
+  for (int k = 0; k < OST; ++k)
+    v[k] = *reinterpret_cast<const float4*>(img + (k * RPK + r0) * ors + d * 4);
+  if (full) {
+    float* dst = obase + (int64_t)(q0 + r0) * p.o_ss + d;
+    const int64_t step = (int64_t)RPK * p.o_ss;
+#pragma unroll
+    for (int k = 0; k < OST; ++k) st_o4<NT>(dst + k * step, v[k].x, v[k].y, v[k].z, v[k].w);
+  } else {
+#pragma unroll
+    for (int k = 0; k < OST; ++k) {
+      const int r = k * RPK + r0;
+      if (q0 + r < p.R && d < p.D)
+        st_o4<NT>(obase + (int64_t)(q0 + r) * p.o_ss + d, v[k].x, v[k].y, v[k].z, v[k].w);
+    }
+  }
+}
+
 template <int DP, bool NT = false>
 __device__ __forceinline__ void store_o_l(const FwdParams& p, const f32x16 (&o)[DP / 32],
                                           float m, float l, int b, int h, int qi, int hh) {

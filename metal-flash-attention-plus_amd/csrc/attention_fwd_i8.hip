@@ -17,8 +17,7 @@
 // Layout: K and V tiles [key][d] int8 in LDS (XOR-swizzled 16-byte chunks).  K is read by rows;
 // V through ds_read_b64_tr_b8, whose lanes pick the keys in the order of the S accumulator
 // registers, so P'^T feeds O^T += V^T·P'^T straight from registers.
-#include "mfa_stage.h"
-#include "mfa_dispatch.h"
+#include "attention_fwd2.h"
 
 namespace mfa {
 
@@ -316,16 +315,11 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
     float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
     const int qb0 = NG * (bid / BH) * BQ;
 #pragma unroll
-    for (int blk = 0; blk < NG; ++blk)
-#pragma unroll
-      for (int k = 0; k < OST; ++k) {
-        const int idx = k * NT + tid;
-        const int r = idx / CPR, d = (idx % CPR) * 4;
-        if (qb0 + blk * BQ + r < p.R && d < p.D)
-          __builtin_nontemporal_store(
-              *reinterpret_cast<const f4v*>(smem + (blk * BQ + r) * ORS + d * 4),
-              reinterpret_cast<f4v*>(obase + (int64_t)(qb0 + blk * BQ + r) * p.o_ss + d));
-      }
+    for (int blk = 0; blk < NG; ++blk) {
+      const int qb = qb0 + blk * BQ;
+      store_o_image<DP, BQ, NT, true>(p, obase, smem + blk * BQ * ORS, ORS, qb, tid,
+                                      qb + BQ <= p.R && p.D == DP);
+    }
     return;
   }
   if (qvalid) {

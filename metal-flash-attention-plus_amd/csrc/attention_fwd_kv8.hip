@@ -170,15 +170,8 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int qb = (2 * pi + blk) * BQ;
-#pragma unroll
-    for (int k = 0; k < OST; ++k) {
-      const int idx = k * NT + tid;
-      const int r = idx / CPR, d = (idx % CPR) * 4;
-      if (qb + r < p.R && d < p.D) {
-        const float4 v = *reinterpret_cast<const float4*>(smem + (blk * 128 + r) * ORS + d * 4);
-        st_o4<true>(obase + (int64_t)(qb + r) * p.o_ss + d, v.x, v.y, v.z, v.w);
-      }
-    }
+    store_o_image<DP, 128, NT, true>(p, obase, smem + blk * 128 * ORS, ORS, qb, tid,
+                                     qb + BQ <= p.R && p.D == DP);
   }
 }
 

@@ -384,7 +384,8 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // LDS-DMA like the tiles (group 0 into the Q staging, group 1 into ring 1, unused before
 // phase 2) so that every prologue load is counted by hand — and step 0 waits for V0 between
 // its softmax and its PV.
-template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false>
+template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false,
+          bool SWFIRST = false>
 __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   constexpr int NT = 256, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
@@ -414,6 +415,8 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const float c = p.c_log2;
   const int wsz = 0x3fffffff;
+  MFA_STAMP(0);
+  MFA_CYC(0);
 
   DmaA<DP, BK, NT> kd, vd;         // a group's own tiles
   DmaA<DP, BK, 2 * NT> ksh, vsh;   // shared tiles, staged by all 8 waves
@@ -487,16 +490,19 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     constexpr bool FIRST = decltype(first_c)::value;  // step 0 of the deferred-V prologue
     // Stage the next step's tile(s) into the slot read two steps ago.
     const int nx = (s + 1) & 1;
-    if (s + 1 < nA) {
-      ksh.issue(khead, b0 + (s + 1) * BK, sk + nx * TILEB);
-      vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
-    } else {
-      int tn;
-      if (tile(s + 1, tn)) {
-        kd.issue(khead, tn, kb0 + nx * TILEB);
-        vd.issue(vhead, tn, vb0 + nx * TILEB);
+    auto stage_next = [&]() {
+      if (s + 1 < nA) {
+        ksh.issue(khead, b0 + (s + 1) * BK, sk + nx * TILEB);
+        vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
+      } else {
+        int tn;
+        if (tile(s + 1, tn)) {
+          kd.issue(khead, tn, kb0 + nx * TILEB);
+          vd.issue(vhead, tn, vb0 + nx * TILEB);
+        }
       }
-    }
+    };
+    if (!(SWFIRST && sw)) stage_next();
     if (sw) {
       // A is complete: its O and L leave from registers (the next tiles' DMA is older than
       // these stores, so the step's counted wait below leaves them in flight).
@@ -510,9 +516,11 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
         // so each store instruction covers 4 rows x DP*2 contiguous bytes (row-per-lane stores
         // touched 32 rows x 32 B); wave-private, so no barrier.  Same store count (NSW).
         char* const wreg = qstg;  // this wave's staging region
+        MFA_STAMP(4);
 #pragma unroll
         for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(wreg, rbase, 0, ds);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): Q is in registers
+        MFA_STAMP(5);
         constexpr int HB = DP * 2, NCH = DP / 8;  // bytes and 16-byte chunks per half-row
         const float inv = p.o_mul / l;
         const int qa0 = q0 + wg * 32;
@@ -531,18 +539,33 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
             }
           __builtin_amdgcn_s_waitcnt(0xC07F);
           constexpr int RPI = 64 / NCH;  // rows per read instruction
+          constexpr int NK = 32 / RPI;
+          const int rl = lane / NCH, j = lane % NCH;
+          float4 v[NK];
 #pragma unroll
-          for (int k = 0; k < 32 / RPI; ++k) {
-            const int r = k * RPI + lane / NCH, j = lane % NCH;
-            const float4 v =
-                *reinterpret_cast<const float4*>(wreg + r * HB + ((j ^ (r & (NCH - 1))) * 16));
-            const int col = half * (DP / 2) + 4 * j;
-            if (qa0 + r < p.R && col < p.D)
-              st_o4<NTS>(obase + (int64_t)(qa0 + r) * p.o_ss + col, v.x, v.y, v.z, v.w);
+          for (int k = 0; k < NK; ++k) {
+            const int r = k * RPI + rl;
+            v[k] = *reinterpret_cast<const float4*>(wreg + r * HB + ((j ^ (r & (NCH - 1))) * 16));
+          }
+          const int col = half * (DP / 2) + 4 * j;
+          if (full_sw) {
+            // Whole block: unguarded stores, the row address advanced by a constant.
+            float* dst = obase + (int64_t)(qa0 + rl) * p.o_ss + col;
+            const int64_t rstep = (int64_t)RPI * p.o_ss;
+#pragma unroll
+            for (int k = 0; k < NK; ++k) st_o4<NTS>(dst + k * rstep, v[k].x, v[k].y, v[k].z, v[k].w);
+          } else {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+              const int r = k * RPI + rl;
+              if (qa0 + r < p.R && col < p.D)
+                st_o4<NTS>(obase + (int64_t)(qa0 + r) * p.o_ss + col, v[k].x, v[k].y, v[k].z, v[k].w);
+            }
           }
           __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next half's writes
         }
         if (hh == 0 && qi < p.R) store_l(p, st.m + __log2f(l), b, h, qi);
+        MFA_STAMP(6);
         __asm__ __volatile__("" ::: "memory");
         q0 = rbB * BQ;
         qi = q0 + wg * 32 + l32;
@@ -556,6 +579,7 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
       }
       prescale_q2<E, DP>(qf, c);
       st.init();
+      if constexpr (SWFIRST) stage_next();  // the switch stores go ahead of the next tiles
     }
     int tc;
     if (tile(s, tc)) {
@@ -577,12 +601,13 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
         fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh);
       }
     }
-    if (sw && full_sw)
+    if (!SWFIRST && sw && full_sw)
       __builtin_amdgcn_s_waitcnt(0x0F70 | (NSW & 15) | ((NSW >> 4) << 14));
     else
       wait_vm();
     __syncthreads();
   };
+  MFA_STAMP(1);
   // Phase 1 up to its last step, which also stages B's Q rows; group 0 switches at step nA.
   int s = 0;
   using F0 = std::false_type;
@@ -591,9 +616,11 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   if (nA > 0 && n2 > 0) {
     if (g == 0) qd.issue(qhead, rbB * BQ + wg * 32, qstg);
     step(s++, false, F0());
+    MFA_STAMP(2);
     step(s++, g == 0, F0());
   }
   for (; s < S; ++s) step(s, false, F0());
+  MFA_STAMP(3);
 
   char* const mbase = smem;  // the rings are free: merge area, then the O row image
   if (n2 == 0) {
@@ -619,15 +646,8 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
         const int qb = (blk ? rbB : rbA) * BQ;
-#pragma unroll
-        for (int k = 0; k < OST; ++k) {
-          const int idx = k * 2 * NT + tid;
-          const int r = idx / CPR, d = (idx % CPR) * 4;
-          if (qb + r < p.R && d < p.D) {
-            const float4 v = *reinterpret_cast<const float4*>(smem + (blk * 128 + r) * ORS + d * 4);
-            st_o4<NTS>(obase + (int64_t)(qb + r) * p.o_ss + d, v.x, v.y, v.z, v.w);
-          }
-        }
+        store_o_image<DP, 128, 2 * NT, NTS>(p, obase, smem + blk * 128 * ORS, ORS, qb, tid,
+                                            qb + BQ <= p.R && p.D == DP);
       }
       return;
     }
@@ -678,16 +698,10 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   }
   __syncthreads();
   float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
-#pragma unroll
-  for (int k = 0; k < OST; ++k) {
-    const int idx = k * 2 * NT + tid;
-    const int r = idx / CPR, d = (idx % CPR) * 4;
-    if (q0 + r < p.R && d < p.D) {
-      const float4 v = *reinterpret_cast<const float4*>(mbase + r * ORS + d * 4);
-      float4* dst = reinterpret_cast<float4*>(obase + (int64_t)(q0 + r) * p.o_ss + d);
-      st_o4<NTS>(reinterpret_cast<float*>(dst), v.x, v.y, v.z, v.w);
-    }
-  }
+  store_o_image<DP, 128, 2 * NT, NTS>(p, obase, mbase, ORS, q0, tid, q0 + BQ <= p.R && p.D == DP);
+  MFA_CYC(1);
+  MFA_STAMP_DRAIN();
+  MFA_STAMP(7);
 }
 
 template <class E, int DP, int BK, bool MIRROR = true>
@@ -715,6 +729,10 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   if (MIRROR && !(dvv && dvv[0] == '0') && !(nt && nt[0] == '0')) {
     if (swi && swi[0] == '0')
       return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, false, true>,
+                    dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
+    const char* swf = getenv("MFA_SHARE_SWFIRST");
+    if (swf && swf[0] == '1')
+      return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true, true, true>,
                     dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
     return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true, true>,
                   dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);

@@ -191,6 +191,28 @@ int main(int argc, char** argv) {
     printf("xcd %d: loop med %7.2f max %7.2f | loop end med %7.2f max %7.2f (n=%zu)\n", x,
            lt[lt.size() / 2], lt.back(), le[le.size() / 2], le.back(), lt.size());
   }
+  if (var[0] == 'p' && causal) {
+    // Shared-tile mirrored pairs: per pair index pi (workgroup / (B·H)), the median over its
+    // workgroups' waves of phase 1 (slot 1 -> 2: the nA shared steps) and phase 2 (slot 2 -> 3:
+    // the switch step and the rest of B's tiles) per step, and the loop end (slot 3).
+    const int nb = (S + 127) / 128, np = (nb + 1) / 2;
+    for (int pi = 0; pi < np; ++pi) {
+      const int nA = 2 * (pi + 1), nBt = 2 * (nb - pi), h0 = (nBt - nA + 1) / 2;
+      std::vector<double> p1, p2, le;
+      for (int w = 0; w < (1 << 17); ++w) {
+        if (!stamps[w * 8] || !stamps[w * 8 + 3]) continue;
+        if ((w / 8) / (B * H) != pi) continue;
+        if (stamps[w * 8 + 2]) {
+          p1.push_back((stamps[w * 8 + 2] - stamps[w * 8 + 1]) / 100.0 / nA);
+          if (h0 > 0) p2.push_back((stamps[w * 8 + 3] - stamps[w * 8 + 2]) / 100.0 / h0);
+        }
+        le.push_back((stamps[w * 8 + 3] - t0) / 100.0);
+      }
+      auto med = [](std::vector<double> a) { if (a.empty()) return 0.0; std::sort(a.begin(), a.end()); return a[a.size() / 2]; };
+      printf("pair %2d: nA %2d phase-2 steps %2d | us/step phase 1 %.3f phase 2 %.3f | loop end med %.2f\n",
+             pi, nA, h0, med(p1), med(p2), med(le));
+    }
+  }
   if (wpb == 4) {
     // Single-block kernel: shader-cycle totals per wave of DMA issue / tile / wait+barrier.
     double a[3] = {0, 0, 0};
