@@ -384,8 +384,7 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // LDS-DMA like the tiles (group 0 into the Q staging, group 1 into ring 1, unused before
 // phase 2) so that every prologue load is counted by hand — and step 0 waits for V0 between
 // its softmax and its PV.
-template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false,
-          bool SWFIRST = false>
+template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false>
 __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   constexpr int NT = 256, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
@@ -490,19 +489,16 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     constexpr bool FIRST = decltype(first_c)::value;  // step 0 of the deferred-V prologue
     // Stage the next step's tile(s) into the slot read two steps ago.
     const int nx = (s + 1) & 1;
-    auto stage_next = [&]() {
-      if (s + 1 < nA) {
-        ksh.issue(khead, b0 + (s + 1) * BK, sk + nx * TILEB);
-        vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
-      } else {
-        int tn;
-        if (tile(s + 1, tn)) {
-          kd.issue(khead, tn, kb0 + nx * TILEB);
-          vd.issue(vhead, tn, vb0 + nx * TILEB);
-        }
+    if (s + 1 < nA) {
+      ksh.issue(khead, b0 + (s + 1) * BK, sk + nx * TILEB);
+      vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
+    } else {
+      int tn;
+      if (tile(s + 1, tn)) {
+        kd.issue(khead, tn, kb0 + nx * TILEB);
+        vd.issue(vhead, tn, vb0 + nx * TILEB);
       }
-    };
-    if (!(SWFIRST && sw)) stage_next();
+    }
     if (sw) {
       // A is complete: its O and L leave from registers (the next tiles' DMA is older than
       // these stores, so the step's counted wait below leaves them in flight).
@@ -579,7 +575,6 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
       }
       prescale_q2<E, DP>(qf, c);
       st.init();
-      if constexpr (SWFIRST) stage_next();  // the switch stores go ahead of the next tiles
     }
     int tc;
     if (tile(s, tc)) {
@@ -601,7 +596,7 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
         fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh);
       }
     }
-    if (!SWFIRST && sw && full_sw)
+    if (sw && full_sw)
       __builtin_amdgcn_s_waitcnt(0x0F70 | (NSW & 15) | ((NSW >> 4) << 14));
     else
       wait_vm();
@@ -729,10 +724,6 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   if (MIRROR && !(dvv && dvv[0] == '0') && !(nt && nt[0] == '0')) {
     if (swi && swi[0] == '0')
       return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, false, true>,
-                    dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
-    const char* swf = getenv("MFA_SHARE_SWFIRST");
-    if (swf && swf[0] == '1')
-      return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true, true, true>,
                     dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
     return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true, true>,
                   dim3(npairs * p.B * p.H), dim3(512), LDS, stream, q);
