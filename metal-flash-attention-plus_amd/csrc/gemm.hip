@@ -357,6 +357,154 @@ static hipError_t launch_gemm2(const GemmParams& p0, int batch, hipStream_t stre
   return launch(mfa_gemm2_kernel<E, 3>, grid, dim3(256), LDS, stream, p);
 }
 
+constexpr int64_t kGemm3MinTiles = 256;  // one workgroup per CU
+
+// NN whole tiles of 256 x 256 (M % 256 == N % 256 == 0, K % 64 == 0), 16-bit operands: one
+// 512-thread workgroup per CU, 8 waves of 128 m x 64 n (two per SIMD).  Same layout as
+// mfa_gemm2_kernel<E, 3> (A by 16-byte row reads, B by transposed reads in the natural k
+// order, D^T computed so the lane is m), with each staged 64-deep k-step serving 256 x 256
+// outputs: half the LDS-DMA bytes per FLOP of the 128 x 128 kernel, and 8 MFMAs per 6 fragment
+// reads instead of 4 per 4.  For the MLA decompression ([B·S, 512] x [512, H·D], two outputs)
+// the grid is one round of the chip instead of two.
+template <class E>
+__global__ void __launch_bounds__(512, 1) mfa_gemm3_kernel(GemmParams p) {
+  constexpr int BM = 256, BN = 256, BK = 64;
+  using TAa = TileA<BK>;   // A tile: 256 rows of 64 k (128 B)
+  using TBb = TileA<BN>;   // B tile: 64 rows of 256 n (512 B)
+  using AB = Arith16<E, BN>;
+  constexpr int ATILE = BM * BK * 2, BTILE = BK * BN * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const ab = smem;
+  char* const bb = smem + 2 * ATILE;
+
+  const int z = blockIdx.z;
+  const char* A = (const char*)p.a + (p.b[1] ? 0 : z * p.sa * 2);
+  const char* B = (const char*)(p.b[1] ? p.b[z] : p.b[0]) + (p.b[1] ? 0 : z * p.sb * 2);
+  char* C = (char*)(p.b[1] ? p.c[z] : p.c[0]);
+  const int64_t coff = p.b[1] ? 0 : z * p.sc;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int rb[2] = {TAa::row_base(l32, hh, 0), TAa::row_base(l32, hh, 1)};
+  const int trn[2] = {TBb::tr_base_nat(lane, 0), TBb::tr_base_nat(lane, 1)};
+
+  DmaA<BK, BM, 512> ad;
+  DmaA<BN, BK, 512> bd;
+  ad.init(p.lda * 2, BM, BK * 2, tid);
+  bd.init(p.ldb * 2, BK, BN * 2, tid);
+  const char* ahead = A + (int64_t)m0 * p.lda * 2;
+  const char* bhead = B + (int64_t)n0 * 2;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+
+  ad.issue(ahead, 0, ab);
+  bd.issue(bhead, 0, bb);
+  wait_vm();
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < p.K; k0 += BK) {
+    if (k0 + BK < p.K) {
+      ad.issue(ahead + (int64_t)(k0 + BK) * 2, 0, ab + (cur ^ 1) * ATILE);
+      bd.issue(bhead + (int64_t)(k0 + BK) * p.ldb * 2, 0, bb + (cur ^ 1) * BTILE);
+    }
+    const char* at = ab + cur * ATILE;
+    const char* bt = bb + cur * BTILE;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      i16x8 af[4], bf[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const i16x8*>(TAa::row_addr(at, rb, 4 * wm + i, s));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = AB::read_tr_nat(bt, trn, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = E::mma(bf[j], af[i], acc[i][j]);
+    }
+    wait_vm();
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // acc[i][j][r] = C[m = m0 + wm*128 + 32i + l32][n = n0 + wn*64 + 32j + acc_row(r, hh)].
+  if (p.c_img) {
+    // 16-bit C through a [256 m][256 n] LDS image (row pitch 528 B) over the released ring,
+    // then whole 512-B rows from all 512 threads.
+    constexpr int CP = BN * 2 + 16;
+    const bool f16c = p.prec_c == P_FP16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x16& a = acc[i][j];
+          auto cv = [&](float x) -> uint32_t {
+            return f16c ? (uint32_t)f32_to_f16(x) : (uint32_t)f32_to_bf16(x);
+          };
+          const uint32_t w0 = cv(a[4 * g]) | (cv(a[4 * g + 1]) << 16);
+          const uint32_t w1 = cv(a[4 * g + 2]) | (cv(a[4 * g + 3]) << 16);
+          const int row = wm * 128 + i * 32 + l32, col = wn * 64 + j * 32 + 8 * g + 4 * hh;
+          *reinterpret_cast<uint2*>(smem + row * CP + col * 2) = make_uint2(w0, w1);
+        }
+    __syncthreads();
+    const int c16 = tid & 31;
+    uint4 v[BM / 16];
+#pragma unroll
+    for (int it = 0; it < BM / 16; ++it)
+      v[it] = *reinterpret_cast<const uint4*>(smem + (it * 16 + (tid >> 5)) * CP + c16 * 16);
+    uint16_t* dst = reinterpret_cast<uint16_t*>(C) + coff + (int64_t)(m0 + (tid >> 5)) * p.ldc + n0 + c16 * 8;
+#pragma unroll
+    for (int it = 0; it < BM / 16; ++it)
+      *reinterpret_cast<uint4*>(dst + (int64_t)it * 16 * p.ldc) = v[it];
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 128 + i * 32 + l32;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 64 + j * 32 + 8 * g + 4 * hh;
+        const int64_t ci = coff + (int64_t)m * p.ldc + n;
+        const f32x16& a = acc[i][j];
+        if (p.prec_c == P_FP32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + ci) =
+              make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
+        } else {
+          auto cv = [&](float x) -> uint32_t {
+            return p.prec_c == P_FP16 ? (uint32_t)f32_to_f16(x) : (uint32_t)f32_to_bf16(x);
+          };
+          const uint32_t w0 = cv(a[4 * g]) | (cv(a[4 * g + 1]) << 16);
+          const uint32_t w1 = cv(a[4 * g + 2]) | (cv(a[4 * g + 3]) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + ci) = make_uint2(w0, w1);
+        }
+      }
+  }
+}
+
+template <class E>
+static hipError_t launch_gemm3(const GemmParams& p0, int batch, hipStream_t stream) {
+  constexpr int RING = 2 * (256 * 64 * 2) + 2 * (64 * 256 * 2);
+  constexpr int IMG = 256 * (256 * 2 + 16);
+  constexpr int LDS = RING > IMG ? RING : IMG;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  const dim3 grid(p0.N / 256, p0.M / 256, batch);
+  GemmParams p = p0;
+  auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
+  p.c_img = p.prec_c != P_FP32 && (p.ldc & 7) == 0 && (p.b[1] || (p.sc & 7) == 0) &&
+            al16(p.c[0]) && al16(p.c[1]);
+  return launch(mfa_gemm3_kernel<E>, grid, dim3(512), LDS, stream, p);
+}
+
 static bool gemm2_eligible(const GemmParams& p) {
   if (const char* e = getenv("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return false;
@@ -383,6 +531,18 @@ hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_
     return hipErrorNotSupported;
   }
   if (gemm2_eligible(p)) {
+    // NN with 256 x 256 whole tiles filling at least one round of the chip: the 8-wave kernel
+    // (4096^3 fp16 1140 vs 932 TF; with fewer tiles than CUs the 128 x 128 kernel's 4x the
+    // workgroups win, e.g. a single [4096, 512] x [512, 2048] 15.0 vs 20.1 us).  MFA_GEMM3=0 /
+    // =1 forces gemm2 / gemm3 (A/B, tests).
+    const char* g3 = getenv("MFA_GEMM3");
+    const int64_t tiles3 = (int64_t)(p.M / 256) * (p.N / 256) * batch;
+    const bool use3 = p.M % 256 == 0 && p.N % 256 == 0 &&
+                      (g3 ? g3[0] == '1' : tiles3 >= kGemm3MinTiles);
+    if (use3) {
+      if (prec_ab == P_FP16) return launch_gemm3<F16>(p, batch, stream);
+      if (prec_ab == P_BF16) return launch_gemm3<BF16>(p, batch, stream);
+    }
     if (prec_ab == P_FP16) return launch_gemm2<F16>(p, batch, stream);
     if (prec_ab == P_BF16) return launch_gemm2<BF16>(p, batch, stream);
   }
@@ -396,6 +556,8 @@ hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_
   return hipGetLastError();
 }
 
+template __global__ void mfa_gemm3_kernel<F16>(GemmParams);
+template __global__ void mfa_gemm3_kernel<BF16>(GemmParams);
 template __global__ void mfa_gemm2_kernel<F16, 0>(GemmParams);
 template __global__ void mfa_gemm2_kernel<BF16, 0>(GemmParams);
 template __global__ void mfa_gemm2_kernel<F16, 1>(GemmParams);
@@ -486,6 +648,20 @@ extern "C" mfa_status_t mfa_gemm_kernel_descriptor(const mfa_gemm_descriptor_t* 
     out->threadgroup_memory_allocation = 2 * (128 * 64 * 2 + 64 * 128 * 2);
     snprintf(out->variant, sizeof(out->variant), "mfa_gemm2_kernel<%s,%s>/mfa_gemm_general_kernel",
              cn, d->transpose_a ? "TN" : "NT");
+  } else if (pl.tuned && !d->load_previous_c && d->M % 256 == 0 && d->N % 256 == 0 &&
+             d->K % 64 == 0 && d->K > 0 && pl.lda % 8 == 0 && pl.ldb % 8 == 0 && pl.ldc % 8 == 0 &&
+             (int64_t)(d->M / 256) * (d->N / 256) * (d->batch ? d->batch : 1) >= mfa::kGemm3MinTiles) {
+    // Whole 256 x 256 tiles (16-byte aligned buffers): the 8-wave LDS-DMA kernel.
+    out->block_m = 256;
+    out->block_n = 256;
+    out->block_k = 64;
+    out->splits_m = 2;
+    out->splits_n = 4;
+    out->threadgroup_size = 512;
+    out->grid_x = d->N / 256;
+    out->grid_y = d->M / 256;
+    out->threadgroup_memory_allocation = 256 * (256 * 2 + 16);
+    snprintf(out->variant, sizeof(out->variant), "mfa_gemm3_kernel<%s>/mfa_gemm_kernel<%s>", cn, cn);
   } else if (pl.tuned) {
     out->threadgroup_memory_allocation = 2 * (128 * 32 * 2 + 32 * 128 * 2);
     snprintf(out->variant, sizeof(out->variant), "mfa_gemm_kernel<%s>/mfa_gemm2_kernel<%s>", cn, cn);

@@ -213,12 +213,13 @@ def test_zero_k_and_empty(gpu):
     assert torch.all(c2 == 3.0)
 
 
-@pytest.mark.parametrize("img", ["1", "0"])
+@pytest.mark.parametrize("kern,img", [("gemm3", "1"), ("gemm2", "1"), ("gemm2", "0")])
 @pytest.mark.parametrize("prec,pc", [(P.FP16, P.FP16), (P.BF16, P.BF16), (P.FP16, P.FP32)])
-def test_whole_tile_c_image_padded_ldc(gpu, prec, pc, img):
-    # A 16-bit C leaves mfa_gemm2_kernel through an LDS image as whole rows (default) or as
-    # per-lane pieces (MFA_GEMM_IMG=0); C has a padded leading dimension whose padding, and the
-    # rows past M, must stay untouched (NaN sentinels).
+def test_whole_tile_c_image_padded_ldc(gpu, prec, pc, kern, img):
+    # A 16-bit C leaves the whole-tile kernels through an LDS image as whole rows (default) or,
+    # on mfa_gemm2_kernel, as per-lane pieces (MFA_GEMM_IMG=0); C has a padded leading dimension
+    # whose padding, and the rows past M, must stay untouched (NaN sentinels).  256 x 256
+    # problems run the 8-wave mfa_gemm3_kernel; MFA_GEMM3=0 keeps mfa_gemm2_kernel.
     Bn, M, N, K, cpad = 2, 256, 256, 128, 8
     rng = np.random.default_rng(12)
     A = rng.standard_normal((Bn, M, K)).astype(np.float32)
@@ -228,11 +229,16 @@ def test_whole_tile_c_image_padded_ldc(gpu, prec, pc, img):
     ldc = N + cpad
     c = torch.full((Bn, M + 1, ldc), float("nan"), dtype=torch.float32, device=DEV).to(TORCH_DTYPE[pc])
     os.environ["MFA_GEMM_IMG"] = img
+    os.environ["MFA_GEMM3"] = "1" if kern == "gemm3" else "0"
     try:
+        mfa.last_launches()
         mfa.gemm(a, b, c, M, N, K, prec, pc, batch=Bn, ldc=ldc, stride_a=M * K, stride_b=K * N,
                  stride_c=(M + 1) * ldc)
+        launched = [r["name"] for r in mfa.last_launches()]
     finally:
         os.environ.pop("MFA_GEMM_IMG", None)
+        os.environ.pop("MFA_GEMM3", None)
+    assert launched and launched[0].startswith(f"mfa_{kern}_kernel<"), launched
     torch.cuda.synchronize()
     got = c.float().cpu().numpy()
     assert np.isnan(got[:, :M, N:]).all() and np.isnan(got[:, M]).all()
@@ -240,5 +246,8 @@ def test_whole_tile_c_image_padded_ldc(gpu, prec, pc, img):
     ref = seen(np.stack([ol.gemm(As[i], Bs[i]) for i in range(Bn)]).astype(np.float32), pc)
     tol = 1e-3 * np.sqrt(K) + (0 if pc == P.FP32 else 8e-3 * np.abs(ref).max())
     assert np.max(np.abs(got[:, :M, :N] - ref)) < tol
+    # The plan names the 8-wave kernel once its 256 x 256 tiles fill a round of the chip.
     d = mfa.gemm_descriptor(M, N, K, prec, pc, batch=Bn, ldc=ldc)
-    assert b"mfa_gemm2_kernel" in mfa.gemm_kernel_descriptor(d).variant
+    assert b"mfa_gemm3_kernel" not in mfa.gemm_kernel_descriptor(d).variant
+    d = mfa.gemm_descriptor(4096, 4096, K, prec, pc)
+    assert b"mfa_gemm3_kernel" in mfa.gemm_kernel_descriptor(d).variant
