@@ -366,12 +366,15 @@ constexpr int64_t kGemm3MinTiles = 256;  // one workgroup per CU
 // outputs: half the LDS-DMA bytes per FLOP of the 128 x 128 kernel, and 8 MFMAs per 6 fragment
 // reads instead of 4 per 4.  For the MLA decompression ([B·S, 512] x [512, H·D], two outputs)
 // the grid is one round of the chip instead of two.
-template <class E>
+// LAY as in mfa_gemm2_kernel: 3 = NN, 1 = NT (B stored [N][K]: both operands k-contiguous
+// images read by rows), 2 = TN (A stored [K][M]: both operands read transposed, permuted order).
+template <class E, int LAY = 3>
 __global__ void __launch_bounds__(512, 1) mfa_gemm3_kernel(GemmParams p) {
   constexpr int BM = 256, BN = 256, BK = 64;
-  using TAa = TileA<BK>;   // A tile: 256 rows of 64 k (128 B)
-  using TBb = TileA<BN>;   // B tile: 64 rows of 256 n (512 B)
+  using TAa = TileA<BK>;   // k-contiguous tile: 256 rows of 64 k (128 B)
+  using TBb = TileA<BN>;   // m/n-contiguous tile: 64 rows of 256 (512 B)
   using AB = Arith16<E, BN>;
+  constexpr bool AK = LAY != 2, BKR = LAY == 1;  // A / B rows are k-contiguous
   constexpr int ATILE = BM * BK * 2, BTILE = BK * BN * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const ab = smem;
@@ -389,13 +392,16 @@ __global__ void __launch_bounds__(512, 1) mfa_gemm3_kernel(GemmParams p) {
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int rb[2] = {TAa::row_base(l32, hh, 0), TAa::row_base(l32, hh, 1)};
   const int trn[2] = {TBb::tr_base_nat(lane, 0), TBb::tr_base_nat(lane, 1)};
+  const int trb[2] = {TBb::tr_base(lane, 0), TBb::tr_base(lane, 1)};
 
-  DmaA<BK, BM, 512> ad;
-  DmaA<BN, BK, 512> bd;
-  ad.init(p.lda * 2, BM, BK * 2, tid);
-  bd.init(p.ldb * 2, BK, BN * 2, tid);
-  const char* ahead = A + (int64_t)m0 * p.lda * 2;
-  const char* bhead = B + (int64_t)n0 * 2;
+  DmaA<AK ? BK : BM, AK ? BM : BK, 512> ad;
+  DmaA<BKR ? BK : BN, BKR ? BN : BK, 512> bd;
+  ad.init(p.lda * 2, AK ? BM : BK, (AK ? BK : BM) * 2, tid);
+  bd.init(p.ldb * 2, BKR ? BN : BK, (BKR ? BK : BN) * 2, tid);
+  const char* ahead = A + (AK ? (int64_t)m0 * p.lda * 2 : (int64_t)m0 * 2);
+  const char* bhead = B + (BKR ? (int64_t)n0 * p.ldb * 2 : (int64_t)n0 * 2);
+  const int64_t astep = AK ? 2 : (int64_t)p.lda * 2;   // bytes per k
+  const int64_t bstep = BKR ? 2 : (int64_t)p.ldb * 2;
 
   f32x16 acc[4][2];
 #pragma unroll
@@ -410,19 +416,33 @@ __global__ void __launch_bounds__(512, 1) mfa_gemm3_kernel(GemmParams p) {
   int cur = 0;
   for (int k0 = 0; k0 < p.K; k0 += BK) {
     if (k0 + BK < p.K) {
-      ad.issue(ahead + (int64_t)(k0 + BK) * 2, 0, ab + (cur ^ 1) * ATILE);
-      bd.issue(bhead + (int64_t)(k0 + BK) * p.ldb * 2, 0, bb + (cur ^ 1) * BTILE);
+      ad.issue(ahead + (int64_t)(k0 + BK) * astep, 0, ab + (cur ^ 1) * ATILE);
+      bd.issue(bhead + (int64_t)(k0 + BK) * bstep, 0, bb + (cur ^ 1) * BTILE);
     }
     const char* at = ab + cur * ATILE;
     const char* bt = bb + cur * BTILE;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       i16x8 af[4], bf[2];
+      if constexpr (LAY == 2) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = *reinterpret_cast<const i16x8*>(TAa::row_addr(at, rb, 4 * wm + i, s));
+        for (int i = 0; i < 4; ++i) af[i] = AB::read_tr_a(at, trb, 32 * (s >> 1), s & 1, wm * 128 + i * 32);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = AB::read_tr_nat(bt, trn, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
+        for (int j = 0; j < 2; ++j) bf[j] = AB::read_tr_a(bt, trb, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = *reinterpret_cast<const i16x8*>(TAa::row_addr(at, rb, 4 * wm + i, s));
+        if constexpr (LAY == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            bf[j] = *reinterpret_cast<const i16x8*>(TAa::row_addr(bt, rb, 2 * wn + j, s));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            bf[j] = AB::read_tr_nat(bt, trn, 32 * (s >> 1), s & 1, wn * 64 + j * 32);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -491,7 +511,7 @@ __global__ void __launch_bounds__(512, 1) mfa_gemm3_kernel(GemmParams p) {
   }
 }
 
-template <class E>
+template <class E, int LAY = 3>
 static hipError_t launch_gemm3(const GemmParams& p0, int batch, hipStream_t stream) {
   constexpr int RING = 2 * (256 * 64 * 2) + 2 * (64 * 256 * 2);
   constexpr int IMG = 256 * (256 * 2 + 16);
@@ -502,7 +522,7 @@ static hipError_t launch_gemm3(const GemmParams& p0, int batch, hipStream_t stre
   auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
   p.c_img = p.prec_c != P_FP32 && (p.ldc & 7) == 0 && (p.b[1] || (p.sc & 7) == 0) &&
             al16(p.c[0]) && al16(p.c[1]);
-  return launch(mfa_gemm3_kernel<E>, grid, dim3(512), LDS, stream, p);
+  return launch(mfa_gemm3_kernel<E, LAY>, grid, dim3(512), LDS, stream, p);
 }
 
 static bool gemm2_eligible(const GemmParams& p) {
@@ -523,23 +543,31 @@ static bool gemm2_eligible(const GemmParams& p) {
   return true;
 }
 
+// 256 x 256 whole tiles filling at least one round of the chip run the 8-wave kernel (4096^3
+// fp16 NN 1140 vs 932 TF; with fewer tiles than CUs the 128 x 128 kernel's 4x the workgroups
+// win, e.g. a single [4096, 512] x [512, 2048] 15.0 vs 20.1 us).  MFA_GEMM3=0 / =1 forces
+// gemm2 / gemm3 (A/B, tests).
+static bool gemm3_pick(const GemmParams& p, int batch) {
+  const char* g3 = getenv("MFA_GEMM3");
+  const int64_t tiles3 = (int64_t)(p.M / 256) * (p.N / 256) * batch;
+  return p.M % 256 == 0 && p.N % 256 == 0 && (g3 ? g3[0] == '1' : tiles3 >= kGemm3MinTiles);
+}
+
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream) {
   if (p.trans_a || p.trans_b) {  // NT / TN: whole tiles on gemm2, else the caller's fallback
     if (!gemm2_eligible(p)) return hipErrorNotSupported;
+    if (gemm3_pick(p, batch)) {
+      if (prec_ab == P_FP16)
+        return p.trans_b ? launch_gemm3<F16, 1>(p, batch, stream) : launch_gemm3<F16, 2>(p, batch, stream);
+      if (prec_ab == P_BF16)
+        return p.trans_b ? launch_gemm3<BF16, 1>(p, batch, stream) : launch_gemm3<BF16, 2>(p, batch, stream);
+    }
     if (prec_ab == P_FP16) return launch_gemm2<F16>(p, batch, stream);
     if (prec_ab == P_BF16) return launch_gemm2<BF16>(p, batch, stream);
     return hipErrorNotSupported;
   }
   if (gemm2_eligible(p)) {
-    // NN with 256 x 256 whole tiles filling at least one round of the chip: the 8-wave kernel
-    // (4096^3 fp16 1140 vs 932 TF; with fewer tiles than CUs the 128 x 128 kernel's 4x the
-    // workgroups win, e.g. a single [4096, 512] x [512, 2048] 15.0 vs 20.1 us).  MFA_GEMM3=0 /
-    // =1 forces gemm2 / gemm3 (A/B, tests).
-    const char* g3 = getenv("MFA_GEMM3");
-    const int64_t tiles3 = (int64_t)(p.M / 256) * (p.N / 256) * batch;
-    const bool use3 = p.M % 256 == 0 && p.N % 256 == 0 &&
-                      (g3 ? g3[0] == '1' : tiles3 >= kGemm3MinTiles);
-    if (use3) {
+    if (gemm3_pick(p, batch)) {
       if (prec_ab == P_FP16) return launch_gemm3<F16>(p, batch, stream);
       if (prec_ab == P_BF16) return launch_gemm3<BF16>(p, batch, stream);
     }
@@ -556,8 +584,12 @@ hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_
   return hipGetLastError();
 }
 
-template __global__ void mfa_gemm3_kernel<F16>(GemmParams);
-template __global__ void mfa_gemm3_kernel<BF16>(GemmParams);
+template __global__ void mfa_gemm3_kernel<F16, 1>(GemmParams);
+template __global__ void mfa_gemm3_kernel<BF16, 1>(GemmParams);
+template __global__ void mfa_gemm3_kernel<F16, 2>(GemmParams);
+template __global__ void mfa_gemm3_kernel<BF16, 2>(GemmParams);
+template __global__ void mfa_gemm3_kernel<F16, 3>(GemmParams);
+template __global__ void mfa_gemm3_kernel<BF16, 3>(GemmParams);
 template __global__ void mfa_gemm2_kernel<F16, 0>(GemmParams);
 template __global__ void mfa_gemm2_kernel<BF16, 0>(GemmParams);
 template __global__ void mfa_gemm2_kernel<F16, 1>(GemmParams);
@@ -642,15 +674,29 @@ extern "C" mfa_status_t mfa_gemm_kernel_descriptor(const mfa_gemm_descriptor_t* 
                       (d->transpose_a != d->transpose_b) && !d->load_previous_c &&
                       d->M % 128 == 0 && d->N % 128 == 0 && d->K % 64 == 0 && d->K > 0 &&
                       pl.lda % 8 == 0 && pl.ldb % 8 == 0 && pl.ldc % 8 == 0;
-  if (tile_t) {
+  const bool big3 = d->M % 256 == 0 && d->N % 256 == 0 &&
+                    (int64_t)(d->M / 256) * (d->N / 256) * (d->batch ? d->batch : 1) >= mfa::kGemm3MinTiles;
+  if (tile_t && big3) {
+    // Whole 256 x 256 tiles, one transpose, filling a round of the chip: the 8-wave kernel.
+    out->block_m = 256;
+    out->block_n = 256;
+    out->block_k = 64;
+    out->splits_m = 2;
+    out->splits_n = 4;
+    out->threadgroup_size = 512;
+    out->grid_x = d->N / 256;
+    out->grid_y = d->M / 256;
+    out->threadgroup_memory_allocation = 256 * (256 * 2 + 16);
+    snprintf(out->variant, sizeof(out->variant), "mfa_gemm3_kernel<%s,%s>/mfa_gemm_general_kernel",
+             cn, d->transpose_a ? "TN" : "NT");
+  } else if (tile_t) {
     // Whole tiles, one transpose: the LDS-DMA kernel (16-byte aligned buffers; the general
     // kernel otherwise).
     out->threadgroup_memory_allocation = 2 * (128 * 64 * 2 + 64 * 128 * 2);
     snprintf(out->variant, sizeof(out->variant), "mfa_gemm2_kernel<%s,%s>/mfa_gemm_general_kernel",
              cn, d->transpose_a ? "TN" : "NT");
-  } else if (pl.tuned && !d->load_previous_c && d->M % 256 == 0 && d->N % 256 == 0 &&
-             d->K % 64 == 0 && d->K > 0 && pl.lda % 8 == 0 && pl.ldb % 8 == 0 && pl.ldc % 8 == 0 &&
-             (int64_t)(d->M / 256) * (d->N / 256) * (d->batch ? d->batch : 1) >= mfa::kGemm3MinTiles) {
+  } else if (pl.tuned && !d->load_previous_c && big3 && d->K % 64 == 0 && d->K > 0 &&
+             pl.lda % 8 == 0 && pl.ldb % 8 == 0 && pl.ldc % 8 == 0) {
     // Whole 256 x 256 tiles (16-byte aligned buffers): the 8-wave LDS-DMA kernel.
     out->block_m = 256;
     out->block_n = 256;

@@ -165,13 +165,16 @@ def test_batched_transposed(gpu, prec, ta, tb):
     assert np.max(np.abs(c.cpu().numpy() - ref)) < tol
 
 
+@pytest.mark.parametrize("kern", ["gemm2", "gemm3"])
 @pytest.mark.parametrize("ta,tb", [(False, True), (True, False)])
 @pytest.mark.parametrize("prec,pc", [(P.FP16, P.FP32), (P.BF16, P.BF16), (P.BF16, P.FP16)])
-def test_whole_tile_transposed_lds_dma(gpu, prec, pc, ta, tb):
+def test_whole_tile_transposed_lds_dma(gpu, prec, pc, ta, tb, kern):
     # NT / TN with equal 16-bit operands and whole 128x128x64 tiles run mfa_gemm2_kernel (both
-    # operands read by rows, or both transposed); C in its own precision; batched, with padded
-    # leading dimensions (NaN padding catches any read outside the logical matrices).
-    Bn, M, N, K, pad = 2, 256, 384, 192, 8
+    # operands read by rows, or both transposed); whole 256x256 tiles the 8-wave
+    # mfa_gemm3_kernel (forced here at a size below one round of the chip); C in its own
+    # precision; batched, with padded leading dimensions (NaN padding catches any read outside
+    # the logical matrices).
+    Bn, M, N, K, pad = (2, 256, 384, 192, 8) if kern == "gemm2" else (2, 256, 512, 192, 8)
     rng = np.random.default_rng(11)
     A = rng.standard_normal((Bn, M, K)).astype(np.float32)
     Bm = rng.standard_normal((Bn, K, N)).astype(np.float32)
@@ -185,8 +188,15 @@ def test_whole_tile_transposed_lds_dma(gpu, prec, pc, ta, tb):
     a = torch.from_numpy(a_full).to(DEV).to(TORCH_DTYPE[prec])
     b = torch.from_numpy(b_full).to(DEV).to(TORCH_DTYPE[prec])
     c = torch.full((Bn, M, N), float("nan"), dtype=torch.float32, device=DEV).to(TORCH_DTYPE[pc])
-    mfa.gemm(a, b, c, M, N, K, prec, pc, transpose_a=ta, transpose_b=tb, batch=Bn,
-             lda=lda, ldb=ldb, stride_a=a_full[0].size, stride_b=b_full[0].size, stride_c=M * N)
+    os.environ["MFA_GEMM3"] = "1" if kern == "gemm3" else "0"
+    try:
+        mfa.last_launches()
+        mfa.gemm(a, b, c, M, N, K, prec, pc, transpose_a=ta, transpose_b=tb, batch=Bn,
+                 lda=lda, ldb=ldb, stride_a=a_full[0].size, stride_b=b_full[0].size, stride_c=M * N)
+        launched = [r["name"] for r in mfa.last_launches()]
+    finally:
+        os.environ.pop("MFA_GEMM3", None)
+    assert launched and launched[0].startswith(f"mfa_{kern}_kernel<"), launched
     torch.cuda.synchronize()
     As, Bs = seen(A, prec), seen(Bm, prec)
     ref = seen(np.stack([ol.gemm(As[i], Bs[i]) for i in range(Bn)]).astype(np.float32), pc)
@@ -197,6 +207,8 @@ def test_whole_tile_transposed_lds_dma(gpu, prec, pc, ta, tb):
     d = mfa.gemm_descriptor(M, N, K, prec, pc, transpose_a=ta, transpose_b=tb, batch=Bn,
                             lda=lda, ldb=ldb)
     assert b"mfa_gemm2_kernel" in mfa.gemm_kernel_descriptor(d).variant
+    d = mfa.gemm_descriptor(4096, 4096, K, prec, pc, transpose_a=ta, transpose_b=tb)
+    assert b"mfa_gemm3_kernel" in mfa.gemm_kernel_descriptor(d).variant
 
 
 def test_zero_k_and_empty(gpu):
