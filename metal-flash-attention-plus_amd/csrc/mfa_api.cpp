@@ -42,6 +42,26 @@ mfa_status_t hip_status(hipError_t e, const char* what) {
   return fail(MFA_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
 }
 
+// Queries over an empty key sequence have no softmax (every row would divide by zero); the
+// reference rejects non-positive sequence lengths when it builds a descriptor
+// (QuantizedAttention.swift:791).  An empty query sequence is a no-op instead.
+mfa_status_t check_keys(int R, int C) {
+  if (R > 0 && C <= 0)
+    return fail(MFA_ERR_INVALID_DESCRIPTOR,
+                "key sequence length %d with %d queries: softmax over no keys", C, R);
+  return MFA_SUCCESS;
+}
+
+// Backward over an empty query sequence: dK = dV = 0 (sums over no queries), written with two
+// memsets and no kernel; a plan query records nothing.
+mfa_status_t zero_kv_grads(float* dk, float* dv, size_t elems, hipStream_t stream) {
+  if (elems == 0 || mfa::plan_capture()) return MFA_SUCCESS;
+  if (hipMemsetAsync(dk, 0, elems * sizeof(float), stream) != hipSuccess ||
+      hipMemsetAsync(dv, 0, elems * sizeof(float), stream) != hipSuccess)
+    return fail(MFA_ERR_LAUNCH, "zeroing dK / dV for an empty query sequence");
+  return MFA_SUCCESS;
+}
+
 int precision_size(int p) {
   switch (p) {
     case MFA_PRECISION_FP32: return 4;
@@ -590,12 +610,14 @@ mfa_status_t plan_multihead(const mfa_multihead_descriptor_t* desc, const void* 
 extern "C" mfa_status_t mfa_multihead_forward(const mfa_multihead_descriptor_t* desc,
                                               const mfa_attention_buffers_t* buf,
                                               void* stream) {
-  if (!buf || !buf->Q || !buf->K || !buf->V || !buf->O)
-    return fail(MFA_ERR_INVALID_ARGUMENT, "forward requires Q, K, V, O");
+  if (!buf) return fail(MFA_ERR_INVALID_ARGUMENT, "null buffers");
   MHAPlan pl;
   mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
   if (st != MFA_SUCCESS) return st;
-  if (pl.R == 0) return MFA_SUCCESS;
+  if (pl.R == 0) return MFA_SUCCESS;  // empty Q / O may be null (a zero-size allocation)
+  if ((st = check_keys(pl.R, pl.C)) != MFA_SUCCESS) return st;
+  if (!buf->Q || !buf->K || !buf->V || !buf->O)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "forward requires Q, K, V, O");
   const mfa_attention_descriptor_t& base = desc->base;
   const int prec = pl.pr.mem[MFA_OPERAND_Q];
 
@@ -761,7 +783,7 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
                                               const mfa_quantized_tensor_t* key,
                                               const mfa_quantized_tensor_t* value, float* output,
                                               void* logsumexp, const void* mask, void* stream) {
-  if (!desc || !output) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  if (!desc) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
   const mfa_attention_descriptor_t& base = desc->base;
   if (!base.has_matrix_dimensions) return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
   const int B = desc->batch_size ? (int)desc->batch_size : 1;
@@ -790,11 +812,14 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     return fail(MFA_ERR_UNSUPPORTED, "K and V must share a precision class");
   if (elem == 0 && (is_quantized(qp) || is_quantized(kp)))
     return fail(MFA_ERR_UNSUPPORTED, "FP32 query with quantized K/V");
+  mfa_status_t st;
+  if (R == 0) return MFA_SUCCESS;  // empty query / output may be null
+  if ((st = check_keys(R, C)) != MFA_SUCCESS) return st;
+  if (!output) return fail(MFA_ERR_INVALID_ARGUMENT, "null output");
 
   mfa::FwdParams p;
   memset(&p, 0, sizeof(p));
   float fq = 1.f, fk = 1.f, fv = 1.f;
-  mfa_status_t st;
   if ((st = quant_operand(query, qp, B, H, R, D, &p.q, &fq, tq)) != MFA_SUCCESS) return st;
   if ((st = quant_operand(key, kp, B, Hkv, C, D, &p.k, &fk, tk)) != MFA_SUCCESS) return st;
   if ((st = quant_operand(value, vp, B, Hkv, C, D, &p.v, &fv, tv)) != MFA_SUCCESS) return st;
@@ -818,7 +843,6 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   p.c_log2 = 1.442695041f * scale * fq * fk;
   p.o_mul = fv;
   if ((st = plan_masks(base, mask, R, C, &p.mask)) != MFA_SUCCESS) return st;
-  if (R == 0) return MFA_SUCCESS;
   if (cfg.integer_matmul && i8mma_eligible(p, elem, qp, kp, vp)) {
     mfa::FwdParams pi = p;
     pi.nblk = (R + 127) / 128;
@@ -950,6 +974,10 @@ bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int 
 mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ksrc, int qsrc,
                           int phase, hipStream_t stream) {
   mfa::BwdParams p = base_p;
+  if (mfa_status_t st = check_keys(p.R, p.C)) return st;
+  if (p.R == 0)
+    return (phase & PHASE_KV) ? zero_kv_grads(p.dk, p.dv, (size_t)p.B * p.Hkv * p.C * p.D, stream)
+                              : MFA_SUCCESS;
   int bp, bt, nw;
   mfa::bwd_block_config(elem, DP, &bp, &bt, &nw);
   const bool big = DP == kBigD;
@@ -987,12 +1015,15 @@ mfa_status_t multihead_backward(const mfa_multihead_descriptor_t* desc,
                                 const mfa_attention_buffers_t* buf, void* stream, int phase) {
   if (!buf) return fail(MFA_ERR_INVALID_ARGUMENT, "null buffers");
   const bool need_q = phase & PHASE_QUERY, need_kv = phase & PHASE_KV;
-  if (!buf->Q || !buf->K || !buf->V || !buf->L || !buf->D || !buf->dO ||
-      (need_q && (!buf->O || !buf->dQ)) || (need_kv && (!buf->dK || !buf->dV)))
-    return fail(MFA_ERR_INVALID_ARGUMENT, "backward requires Q K V O L D dO and the gradients");
   MHAPlan pl;
   mfa_status_t st = plan_multihead(desc, buf->mask, &pl);
   if (st != MFA_SUCCESS) return st;
+  if ((st = check_keys(pl.R, pl.C)) != MFA_SUCCESS) return st;
+  // With no queries only dK / dV are written (zeros); the empty row operands may be null.
+  if (pl.R > 0 ? (!buf->Q || !buf->K || !buf->V || !buf->L || !buf->D || !buf->dO ||
+                  (need_q && (!buf->O || !buf->dQ)) || (need_kv && (!buf->dK || !buf->dV)))
+               : (need_kv && pl.C > 0 && (!buf->dK || !buf->dV)))
+    return fail(MFA_ERR_INVALID_ARGUMENT, "backward requires Q K V O L D dO and the gradients");
   const mfa_attention_descriptor_t& base = desc->base;
   const int prec = pl.pr.mem[MFA_OPERAND_Q];
   mfa::BwdParams p;
@@ -1054,10 +1085,7 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
                                 const void* grad_output, const void* logsumexp,
                                 float* grad_query, float* grad_key, float* grad_value,
                                 void* d_values, int phase, void* stream) {
-  if (!desc || !grad_output || !logsumexp || !d_values)
-    return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
-  if ((phase & PHASE_QUERY) && (!output || !grad_query))
-    return fail(MFA_ERR_INVALID_ARGUMENT, "backwardQuery requires output and gradQuery");
+  if (!desc) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
   if ((phase & PHASE_KV) && (!grad_key || !grad_value))
     return fail(MFA_ERR_INVALID_ARGUMENT, "backwardKeyValue requires gradKey and gradValue");
   const mfa_attention_descriptor_t& base = desc->base;
@@ -1067,6 +1095,15 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   const int Hkv = desc->num_kv_heads ? (int)desc->num_kv_heads : H;
   const int R = (int)base.row, C = (int)base.column, D = (int)base.head;
   if (D <= 0) return fail(MFA_ERR_INVALID_DESCRIPTOR, "head dimension %d", D);
+  if (mfa_status_t st = check_keys(R, C)) return st;
+  if (R == 0)  // no queries: the row operands may be null (zero-size allocations)
+    return (phase & PHASE_KV) ? zero_kv_grads(grad_key, grad_value, (size_t)B * Hkv * C * D,
+                                              (hipStream_t)stream)
+                              : MFA_SUCCESS;
+  if (!grad_output || !logsumexp || !d_values)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  if ((phase & PHASE_QUERY) && (!output || !grad_query))
+    return fail(MFA_ERR_INVALID_ARGUMENT, "backwardQuery requires output and gradQuery");
   const int DP = pad_head(D);
   const bool tr = base.has_transpose_state;
   const bool tq = tr && base.transpose_q, tk = tr && base.transpose_k;
@@ -1326,6 +1363,7 @@ extern "C" mfa_status_t mfa_mla_forward(const mfa_mla_descriptor_t* desc, const 
     if (st != MFA_SUCCESS) return st;
   }
   if (Sq == 0) return MFA_SUCCESS;
+  if ((st = check_keys(Sq, Skv)) != MFA_SUCCESS) return st;
   // Attention on BSHD K/V: element strides [S·H·D, D, H·D, 1].
   const int64_t kv_strides[4] = {(int64_t)Skv * H * D, D, (int64_t)H * D, 1};
   mfa::FwdParams p;
@@ -1424,8 +1462,9 @@ extern "C" mfa_status_t mfa_mla_forward_absorbed(const mfa_mla_descriptor_t* des
   mfa_status_t st0 = check_transposes(desc->base, false, "absorbed MLA forward");
   if (st0 != MFA_SUCCESS) return st0;
   if (Sq == 0) return MFA_SUCCESS;
+  mfa_status_t st = check_keys(Sq, Skv);
+  if (st != MFA_SUCCESS) return st;
   hipStream_t s = (hipStream_t)stream;
-  mfa_status_t st;
   // Q~, O~ and the split-KV partials, carved from the caller's workspace
   // (mfa_mla_absorbed_workspace_size bytes) or from this stream's scratch.
   const AbsorbedLayout al = absorbed_layout(B, H, Sq, Skv, Lat);

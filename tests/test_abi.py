@@ -125,8 +125,12 @@ def test_incompatible_shapes_fail_before_launch():
     b.Q = b.K = b.V = b.O = 16  # never dereferenced: validation fails first
     st = mfa.lib.mfa_multihead_forward(ctypes.byref(bad), ctypes.byref(b), None)
     assert st == 1
-    b2 = mfa.AttentionBuffers()
-    assert mfa.lib.mfa_multihead_forward(ctypes.byref(bad), ctypes.byref(b2), None) == 4
+    b2 = mfa.AttentionBuffers()  # null operands: the descriptor is checked first, then them
+    assert mfa.lib.mfa_multihead_forward(ctypes.byref(bad), ctypes.byref(b2), None) == 1
+    good = mfa.MultiHeadDescriptor.make(base, 2, 8, 64, 32, Hkv=2)
+    assert mfa.lib.mfa_multihead_forward(ctypes.byref(good), ctypes.byref(b2), None) == 4
+    empty = mfa.MultiHeadDescriptor.make(base, 2, 8, 0, 32, C=64)  # no queries: nothing to read
+    assert mfa.lib.mfa_multihead_forward(ctypes.byref(empty), ctypes.byref(b2), None) == 0
 
 
 def test_masking_heuristic_known_answers():

@@ -147,6 +147,17 @@ def test_attention_kernel_reports_dispatched_variant():
 
 def test_empty_shape_plans_nothing():
     assert mfa.multihead_plan(mh(1, 2, 0, 64, C=64)) == []
+    assert mfa.multihead_plan(mh(1, 2, 0, 64, C=0)) == []
+    for kind in (K.backwardQuery, K.backwardKeyValue):
+        assert mfa.multihead_plan(mh(1, 2, 0, 64, C=64), kind) == []  # dK = dV = 0, no kernel
+
+
+@pytest.mark.parametrize("kind", [K.forward, K.backwardQuery, K.backwardKeyValue])
+def test_queries_over_no_keys_rejected(kind):
+    """A softmax over zero keys is undefined; the reference refuses non-positive sequence
+    lengths (QuantizedAttention.swift:791).  The call fails before any launch."""
+    with pytest.raises(mfa.MFAError, match="softmax over no keys"):
+        mfa.multihead_plan(mh(1, 2, 64, 64, C=0), kind)
 
 
 def test_invalid_descriptor_fails_like_the_call():
