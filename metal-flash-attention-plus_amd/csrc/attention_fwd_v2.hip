@@ -27,6 +27,35 @@
 namespace mfa {
 
 // ---------------------------------------------------------------------------------------
+// Rows with no unmasked key (empty sparse range, or a range the causal / window predicates
+// empty).  The reference masks with a finite value (AttentionKernel+Softmax.swift:257), so
+// such a row sees the same score for every key: P = 1, O = Σ_k V_k / C, and L = m + log2 C
+// with m = (mask value)·c as the forward computes it.  The tuned forward masks with -inf and
+// skips tiles, so the wave owning such a row writes it afterwards: lanes across the head
+// dimension, keys summed in order.
+__device__ __forceinline__ bool masked_everywhere(const FwdParams& p, uint32_t x, uint32_t y,
+                                                  int q) {
+  int64_t lo = x, hi = min((int64_t)y, (int64_t)p.C);
+  if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
+  if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
+  return lo >= hi;
+}
+
+template <class E>
+__device__ __forceinline__ void fill_masked_row(const FwdParams& p, int b, int h, int kvh, int q,
+                                                int lane) {
+  const uint16_t* vbase = (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
+  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
+  const float l = (float)p.C;
+  for (int d = lane; d < p.D; d += 64) {
+    float acc = 0.f;
+    for (int k = 0; k < p.C; ++k) acc += E::to_f32(vbase[(int64_t)k * p.v.ss + (int64_t)d * p.v.sd]);
+    orow[(int64_t)d * p.o_sd] = acc * (p.o_mul / l);
+  }
+  if (lane == 0) store_l(p, mul_rn(kMaskValue, p.c_log2) + __log2f(l), b, h, q);
+}
+
+// ---------------------------------------------------------------------------------------
 // One 128-row query block per workgroup (4 waves x 32 rows); WPS workgroups' waves per SIMD.
 template <class E, int DP, int BK, int WPS, class TU = TuneDefault>
 __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
@@ -64,16 +93,18 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   key_range(p, q0, BQ, BK, &kbeg, &kend);
   // Sparse ranges (SparseMQABuilder, AttentionKernel+Softmax.swift:278-304): the row's keys
   // [x, y); tiles outside the union of the block's non-empty ranges are skipped.  Rows left
-  // with no unmasked key are rewritten by mfa_fwd_masked_rows_kernel (the reference's finite
-  // mask value makes them a uniform average over every key).
+  // with no unmasked key are written by their wave after the loop (fill_masked_row: the
+  // reference's finite mask value makes them a uniform average over every key).
   int rlo = -0x40000000, rhi = 0x3fffffff;
   int in_lo = 0, in_hi = 0x3fffffff;  // keys inside every non-empty range of the block
+  bool row_empty = false;
   if (p.mask.ranges) {
     uint32_t x = 0u, y = 0u;
     if (qvalid) {
       const uint32_t* rp = p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + qi);
       x = rp[0];
       y = rp[1];
+      row_empty = masked_everywhere(p, x, y, qi);
     }
     rlo = (int)min(x, 0x3fffffffu);
     rhi = (int)min(y, 0x3fffffffu) - 1;
@@ -162,7 +193,16 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   MFA_STAMP(2);
   float l = cross_half_sum(st.lh) + kFltMin;
   if (!(l > 0.f)) l = kFltMin;
-  if (qvalid) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+  if (qvalid && !row_empty) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+  if (p.mask.ranges) {
+    // The wave writes its rows with no unmasked key itself, one row at a time (rare).
+    uint64_t todo = __ballot(row_empty && hh == 0);
+    while (todo) {
+      const int src = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      fill_masked_row<E>(p, b, h, kvh, q0 + wave * 32 + src, lane);
+    }
+  }
   MFA_STAMP(3);
   MFA_CYC(1);
   MFA_STAMP_DRAIN();
@@ -769,65 +809,6 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
   return launch(kern, dim3(npairs * p.B * p.H), dim3(NWG * 128), LDS, stream, q);
 }
 
-// ---------------------------------------------------------------------------------------
-// Rows with no unmasked key (empty sparse range, or a range the causal / window predicates
-// empty).  The reference masks with a finite value (AttentionKernel+Softmax.swift:257), so
-// such a row sees the same score for every key: P = 1, O = Σ_k V_k / C, and L = m + log2 C
-// with m = (mask value)·c as the forward computes it.  One thread tests each query row; a
-// wave then rewrites its empty rows together.  Runs after the tuned forward, which masks
-// with -inf.
-template <class E>
-__global__ void __launch_bounds__(256) mfa_fwd_masked_rows_kernel(FwdParams p) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nrows = (int64_t)p.B * p.H * p.R;
-  const int64_t rid = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (b·H + h)·R + q
-  bool empty = false;
-  if (rid < nrows) {
-    const int q = (int)(rid % p.R);
-    const int bh = (int)(rid / p.R);
-    const int h = bh % p.H, b = bh / p.H, kvh = h % p.Hkv;
-    const uint32_t* rp = p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + q);
-    int64_t lo = rp[0], hi = min((int64_t)rp[1], (int64_t)p.C);
-    if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
-    if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
-    empty = lo >= hi;
-  }
-  // The wave walks its empty rows together, lanes across the head dimension.
-  uint64_t todo = __ballot(empty);
-  while (todo) {
-    const int src = __builtin_ctzll(todo);
-    todo &= todo - 1;
-    const int64_t r = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63) + src;
-    const int q = (int)(r % p.R);
-    const int bh = (int)(r / p.R);
-    const int h = bh % p.H, b = bh / p.H, kvh = h % p.Hkv;
-    const uint16_t* vbase = (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
-    float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
-    const float l = (float)p.C;
-    for (int d = lane; d < p.D; d += 64) {
-      float acc = 0.f;
-      for (int k = 0; k < p.C; ++k) acc += E::to_f32(vbase[(int64_t)k * p.v.ss + (int64_t)d * p.v.sd]);
-      orow[(int64_t)d * p.o_sd] = acc * (p.o_mul / l);
-    }
-    if (lane == 0) {
-      const float L = mul_rn(kMaskValue, p.c_log2) + __log2f(l);
-      const int64_t li = (int64_t)(b * p.H + h) * p.R + q;
-      if (p.l_f16)
-        reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
-      else
-        reinterpret_cast<float*>(p.l)[li] = L;
-    }
-  }
-}
-
-hipError_t fwd_masked_rows_dispatch(const FwdParams& p, int elem, hipStream_t stream) {
-  const int64_t rows = (int64_t)p.B * p.H * p.R;
-  const dim3 grid((unsigned)((rows + 255) / 256));
-  if (elem == P_FP16) return launch(mfa_fwd_masked_rows_kernel<F16>, grid, dim3(256), 0, stream, p);
-  if (elem == P_BF16) return launch(mfa_fwd_masked_rows_kernel<BF16>, grid, dim3(256), 0, stream, p);
-  return hipErrorNotSupported;
-}
-
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   const char* var = getenv("MFA_FWD_VARIANT");
@@ -838,7 +819,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   bool single = !p.mask.causal || DP > 128 || (blocks > 768 && !(p.nblk >= 64 && blocks <= 1536)) ||
                 p.mask.ranges;
   if (var && var[0] == 's') single = true;
-  if (var && var[0] == 'p') single = false;
+  if (var && var[0] == 'p' && !p.mask.ranges) single = false;
   // Development A/B of the scheduling knobs on the fp16 D=128 single-block kernel.
   if (const char* tv = getenv("MFA_FWD2_TUNE")) {
     if (elem == P_FP16 && DP == 128 && single) {

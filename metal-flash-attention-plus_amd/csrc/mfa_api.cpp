@@ -267,7 +267,7 @@ bool fwd2_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
   if (kvsrc != 0 || (DP != 64 && DP != 128 && DP != 256)) return false;
   if (!(p.c_log2 > 0.f)) return false;
   // Rows that end up masked everywhere need the reference's finite-mask result: with sparse
-  // ranges a fix-up pass rewrites them; otherwise they must not occur (skip_ok).
+  // ranges the kernel writes them after its loop; otherwise they must not occur (skip_ok).
   if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok && !p.mask.ranges) return false;
   if (p.D % 8 != 0 || p.mask.amask) return false;
   if (p.mask.ranges && DP > 128) return false;
@@ -288,7 +288,6 @@ hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, 
   }
   if (fwd2_eligible(p, elem, DP, kvsrc)) {
     hipError_t e = mfa::fwd2_dispatch(p, elem, DP, s);
-    if (e == hipSuccess && p.mask.ranges) e = mfa::fwd_masked_rows_dispatch(p, elem, s);
     if (e != hipErrorNotSupported) return e;
   }
   if (fast_eligible(p, elem, DP, kvsrc)) {

@@ -67,9 +67,6 @@ hipError_t bwd_bigd_dispatch(const BwdParams& p, int kind, int elem, hipStream_t
 // needs (partials of every wave).
 size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D);
 hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hipStream_t stream);
-// Rows with no unmasked key after a sparse-range forward on the tuned kernel: O = mean of V,
-// L as the reference's finite mask value gives it (attention_fwd_v2.hip).
-hipError_t fwd_masked_rows_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 // FP16 Q with per-tensor INT8 / INT4 K/V (src SRC_I8 / SRC_I4) widened on load inside the
 // shared-tile loop (attention_fwd_kv8.hip); D <= 128 padded to 128, no masks.
 hipError_t fwd_kv8_dispatch(const FwdParams& p, int elem, int src, hipStream_t stream);

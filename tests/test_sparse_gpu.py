@@ -4,8 +4,8 @@ The HAS_SPARSE_RANGES mask (AttentionKernel+Softmax.swift:278-304) gives every q
 half-open key range [x, y), indexed (b*H_kv + kv)*R + row; SparseMQABuilder.buildBlockSparse
 (SparseMQABuilder.swift:30-62) turns a block pattern into such ranges.  The tuned kernel skips
 the key tiles outside the union of a query block's ranges; rows left with no unmasked key get
-the reference's finite-mask result (uniform average of V, L = mask*c + log2 C) from a fix-up
-pass.  Tolerances: SquareAttentionTest.swift:557-571 (mixed O 5e-2); L here is kept in fp32
+the reference's finite-mask result (uniform average of V, L = mask*c + log2 C), written by the
+owning wave after the tile loop.  Tolerances: SquareAttentionTest.swift:557-571 (mixed O 5e-2); L here is kept in fp32
 (lowPrecisionIntermediates off) so the fully masked rows' L stays finite.
 """
 import numpy as np
@@ -73,8 +73,7 @@ def test_block_sparse_tuned_kernel(gpu, prec, D):
     Q = gaussian((B, H, S, D), 901)
     K, V = gaussian((B, Hkv, S, D), 902), gaussian((B, Hkv, S, D), 903)
     plan = check(Q, K, V, prec, ranges)
-    assert any("mfa_fwd2_kernel" in n for n in plan), plan
-    assert any("masked_rows" in n for n in plan), plan
+    assert len(plan) == 1 and "mfa_fwd2_kernel" in plan[0], plan  # empty rows in-kernel
 
 
 @pytest.mark.parametrize("causal,window", [(True, None), (False, 90), (False, 300)])
