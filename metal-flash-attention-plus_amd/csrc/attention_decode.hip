@@ -18,7 +18,9 @@
 //     way for O^T += V^T·P^T;
 //   * every wave writes its partial (m, l, unnormalised O) for the valid rows; a merge pass
 //     combines the 4·nsplit partials of each row into O = Σ w_s O_s / Σ w_s l_s and
-//     L = m + log2 l (w_s = exp2(m_s - m)).
+//     L = m + log2 l (w_s = exp2(m_s - m)).  With one split per unit (the B32 H16 decode
+//     rows) the workgroup holds all 4 partials and merges them through LDS itself: one
+//     launch, the same arithmetic in the same order.
 #include "mfa_stage.h"
 #include "mfa_dispatch.h"
 
@@ -29,6 +31,43 @@ typedef int i32x2d __attribute__((ext_vector_type(2)));
 template <class E>
 __device__ __forceinline__ i16x8 widen_i8(uint32_t lo, uint32_t hi, float zp) {
   return __builtin_bit_cast(i16x8, dequant_fast<E, SRC_I8>(make_uint4(lo, hi, 0u, 0u), zp));
+}
+
+// Combines the np partials (m_s, l_s, O_s) of one query row for columns d .. d+3 and stores
+// O = Σ w_s O_s / (Σ w_s l_s + FLT_MIN), w_s = exp2(m_s - max m), and with write_l also
+// L = max m + log2 l.  Partial s is ml[s·mls] and the D floats at op + s·ops (global memory
+// for the merge pass, LDS for the in-workgroup merge).
+__device__ __forceinline__ void merge_partials(const FwdParams& p, const float2* ml, int64_t mls,
+                                               const float* op, int64_t ops, int np, int b,
+                                               int h, int q, int d, bool write_l) {
+  float mx = -kFltMax;
+  for (int s = 0; s < np; ++s) mx = fmaxf(mx, ml[s * mls].x);
+  float l = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < np; ++s) {
+    const float2 m_l = ml[s * mls];
+    const float w = __builtin_amdgcn_exp2f(m_l.x - mx);
+    l += m_l.y * w;
+    if (d < p.D) {
+      const float4 v = *reinterpret_cast<const float4*>(op + s * ops + d);
+      acc.x += v.x * w; acc.y += v.y * w; acc.z += v.z * w; acc.w += v.w * w;
+    }
+  }
+  l += kFltMin;
+  const float inv = p.o_mul / l;
+  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
+  const float vals[4] = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (d + e < p.D) orow[(int64_t)(d + e) * p.o_sd] = vals[e];
+  if (write_l) {
+    const float L = mx + __log2f(l);
+    const int64_t li = (int64_t)(b * p.H + h) * p.R + q;
+    if (p.l_f16)
+      reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+    else
+      reinterpret_cast<float*>(p.l)[li] = L;
+  }
 }
 
 template <class E, int DP>
@@ -190,8 +229,37 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
     }
   }
 
-  // This wave's partial for the tile's valid rows.
   const float l = cross_half_sum(lh);
+  if (dp.fused) {
+    // One split: the 4 waves' partials meet in LDS ([4][32][DP] O, then [4][32] (m, l)),
+    // over the ring once every wave is done with it, and 256 threads merge them.
+    __syncthreads();
+    float* po = reinterpret_cast<float*>(smem);
+    float2* pml = reinterpret_cast<float2*>(smem + 4 * 32 * DP * 4);
+    float* prow = po + (wave * 32 + l32) * DP;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(prow + dt * 32 + 8 * g + 4 * hh) =
+            make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
+    if (hh == 0) pml[wave * 32 + l32] = make_float2(m, l);
+    __syncthreads();
+    constexpr int CH = DP / 4, RPI = 256 / CH;  // 16-byte chunks per row, rows per pass
+    const int ch = tid % CH;
+#pragma unroll
+    for (int k = 0; k < 32 / RPI; ++k) {
+      const int r = tid / CH + k * RPI;
+      const int qr = rt * 32 + r;
+      if (qr < dp.rows) {
+        const int g = qr / p.R, q = qr % p.R;
+        merge_partials(p, pml + r, 32, po + r * DP, 32 * DP, 4, b, kvh + g * p.Hkv, q, 4 * ch,
+                       ch == 0);
+      }
+    }
+    return;
+  }
+  // This wave's partial for the tile's valid rows.
   if (rvalid) {
     const int np = dp.nsplit * 4;
     const int64_t pidx = ((int64_t)u * np + split * 4 + wave) * 32 + l32;
@@ -224,35 +292,8 @@ __global__ void __launch_bounds__(256) mfa_decode_merge_kernel(DecodeParams dp) 
   const int u = (b * p.Hkv + kvh) * dp.nrt + row / 32;
   const int np = dp.nsplit * 4;
   const int64_t base = (int64_t)u * np * 32 + (row % 32);
-  float mx = -kFltMax;
-  for (int s = 0; s < np; ++s) mx = fmaxf(mx, dp.mlpart[base + (int64_t)s * 32].x);
-  float l = 0.f;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int d = 4 * lane;
-  for (int s = 0; s < np; ++s) {
-    const float2 ml = dp.mlpart[base + (int64_t)s * 32];
-    const float w = __builtin_amdgcn_exp2f(ml.x - mx);
-    l += ml.y * w;
-    if (d < p.D) {
-      const float4 v = *reinterpret_cast<const float4*>(dp.opart + (base + (int64_t)s * 32) * p.D + d);
-      acc.x += v.x * w; acc.y += v.y * w; acc.z += v.z * w; acc.w += v.w * w;
-    }
-  }
-  l += kFltMin;
-  const float inv = p.o_mul / l;
-  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
-  const float vals[4] = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-    if (d + e < p.D) orow[(int64_t)(d + e) * p.o_sd] = vals[e];
-  if (lane == 0) {
-    const float L = mx + __log2f(l);
-    const int64_t li = (int64_t)(b * p.H + h) * p.R + q;
-    if (p.l_f16)
-      reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
-    else
-      reinterpret_cast<float*>(p.l)[li] = L;
-  }
+  merge_partials(p, dp.mlpart + base, 32, dp.opart + base * p.D, (int64_t)32 * p.D, np, b, h, q,
+                 4 * lane, lane == 0);
 }
 
 // Split of the key range: enough workgroups for two per CU (512) when the units alone do not
@@ -289,10 +330,14 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
   if (units >= 65536) return hipErrorNotSupported;
   const dim3 grid(dp.nsplit, units, 1);
   const int DP = p.D <= 64 ? 64 : p.D <= 128 ? 128 : 256;
+  // MFA_DECODE_MERGE=1 keeps the separate merge pass for one split too (A/B, tests).
+  const char* mv = getenv("MFA_DECODE_MERGE");
+  dp.fused = dp.nsplit == 1 && !(mv && mv[0] == '1');
   hipError_t e = hipErrorNotSupported;
 #define MFA_DEC(ELEM, EE, DPV)                                                                 \
   if (elem == ELEM && DP == DPV)                                                               \
-    e = launch(mfa_fwd_decode_kernel<EE, DPV>, grid, dim3(256), 4 * 2 * 2 * 32 * DPV, stream, dp);
+    e = launch(mfa_fwd_decode_kernel<EE, DPV>, grid, dim3(256), 4 * 2 * 2 * 32 * DPV + 1024,  \
+               stream, dp);
   MFA_DEC(P_FP16, F16, 64)
   MFA_DEC(P_FP16, F16, 128)
   MFA_DEC(P_FP16, F16, 256)
@@ -300,7 +345,7 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
   MFA_DEC(P_BF16, BF16, 128)
   MFA_DEC(P_BF16, BF16, 256)
 #undef MFA_DEC
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || dp.fused) return e;
   const int64_t nrows = (int64_t)p.B * p.H * p.R;
   return launch(mfa_decode_merge_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, stream, dp);
 }

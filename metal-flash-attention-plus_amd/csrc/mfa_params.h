@@ -76,6 +76,7 @@ struct DecodeParams {
   int32_t chunk;     // keys per split (whole rounds of 4 waves x 32-key tiles)
   float* opart;      // [units][4·nsplit][32][D] unnormalised O of each wave
   float2* mlpart;    // [units][4·nsplit][32] (m, l)
+  int32_t fused;     // nsplit == 1: the workgroup merges its 4 waves' partials in LDS
 };
 
 // MFMA GEMM (gemm.hip): C = A·B (+C); two (B, C) pairs share A when b[1] != nullptr.

@@ -292,3 +292,11 @@ def test_absorbed_workspace_covers_split_partials():
     # Prefill (S_q 4096): enough blocks, no split: Q~ and O~ only.
     pre = mfa.lib.mfa_mla_absorbed_workspace_size(ctypes.byref(mla_desc(1, 16, 4096, 4096, 128, 512)))
     assert pre == 2 * 16 * 4096 * 512 * 2
+
+
+def test_decode_bench_shape_is_one_launch():
+    # The bench's decode rows (B32 H16 S_kv 8192, S_q 1 and 16): one split per unit.
+    for R in (1, 16):
+        base = mfa.AttentionDescriptor.make(R, 8192, 128, low_precision=True, precision=P.FP16)
+        desc = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=32, H=16)
+        assert [r["name"] for r in mfa.quantized_plan(desc)] == ["mfa_fwd_decode_kernel<F16, 128>"]
