@@ -47,6 +47,7 @@ def banded_pattern(nqb, nkb, width, seed, empty_every=0):
 
 
 def check(Q, K, V, prec, ranges, causal=False, window=None):
+    mfa.last_launches()  # drop what earlier tests launched on this thread
     o, l = run_forward(Q, K, V, prec=prec, causal=causal, window=window, ranges=ranges,
                        low_precision_intermediates=False)
     plan = [x["name"] for x in mfa.last_launches()]
