@@ -488,6 +488,7 @@ def test_integer_matmul_c3_heads(gpu):
     (1, 8, 2, 3, 777, 64, P.BF16),     # GQA: 12 rows per kv head
     (2, 4, 1, 5, 300, 256, P.FP16),    # MQA: 20 rows, D 256
     (1, 16, 1, 4, 2048, 128, P.BF16),  # 64 rows per kv head: two row tiles
+    (1, 16, 1, 4, 300, 128, P.FP16),   # two row tiles, one split: in-workgroup merge
     (1, 2, 2, 1, 33, 64, P.FP16),      # one partial tile
 ])
 def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
