@@ -436,13 +436,14 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   BST(7);
 
   int cur = 0;
+  // Step s covers query tile t of query head h = kvh + g·Hkv (g = s / ntile), walked
+  // incrementally: a per-step integer division costs a few hundred cycles of the step.
+  const int qlast = qbeg + (ntile - 1) * BQ;
+  int t = qbeg, h = kvh;
   for (int step = 0; step < nsteps; ++step) {
-    const int g = step / ntile;
-    const int t = qbeg + (step - g * ntile) * BQ;
     const bool has_next = step + 1 < nsteps;
-    const int gn = (step + 1) / ntile;
-    const int tn = qbeg + (step + 1 - gn * ntile) * BQ;
-    const int hn = kvh + gn * p.Hkv;
+    const int tn = t < qlast ? t + BQ : qbeg;
+    const int hn = t < qlast ? h : h + p.Hkv;
     if (has_next) ld_load(hn, tn);
     if (!spread_dma<DP>() && has_next) {
       qd.issue(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB);
@@ -641,6 +642,8 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     __syncthreads();
     BST(6);
     cur ^= 1;
+    t = tn;
+    h = hn;
   }
   BST_END();
 
