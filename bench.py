@@ -483,6 +483,7 @@ def main():
     ran = mfa.last_launches()
     assert len(plan) == 1 and ran and all(r == plan[0] for r in ran), (plan, ran)
     kname = plan[0]["name"]
+    pmc = pmc_record(kname, S, H, D)
     result = {
         "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
         "value": round(value, 2),
@@ -509,7 +510,16 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                      "peak": round(PEAK_FP16_TFLOPS, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-                     "traffic": pmc_traffic(kname, S, H, D),
+                     "traffic": pmc.get("hbm_bytes"),
+                     # north_star's two utilisation figures for the dominant kernel: MFMA busy
+                     # (PMC: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)) and
+                     # achieved HBM GB/s (PMC bytes per launch / this run's kernel time) against
+                     # the ~8 TB/s HBM3E peak.
+                     "mfma_busy": pmc.get("mfma_busy"),
+                     "hbm_GBps": (round(pmc["hbm_bytes"] / (kernel_ms * 1e-3) / 1e9, 1)
+                                  if pmc.get("hbm_bytes") else None),
+                     "hbm_peak_GBps": 8000.0,
+                     "pmc_source": pmc.get("source"),
                      "kernel": kname, "kernel_ms": round(kernel_ms, 4)},
         **result,
     }
@@ -556,19 +566,24 @@ def fake_device_run(args, world: int, rank: int):
         dist_.destroy_process_group()
 
 
-def pmc_traffic(kernel: str, S: int, H: int, D: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md), collected at the default bench shape only; None otherwise."""
+def pmc_record(kernel: str, S: int, H: int, D: int) -> dict:
+    """PMC figures of `kernel` per launch from the newest committed rocprofv3 summary
+    (profiles/r*_pmc_traffic.json, tools/pmc_traffic.py): HBM bytes (2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md) and the MFMA busy fraction;
+    collected at the default bench shape only; {} otherwise."""
     if (S, H, D) != (4096, 16, 128):
-        return None
+        return {}
     import glob
     files = sorted(glob.glob(os.path.join(_REPO, "profiles", "r*_pmc_traffic.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        rec = json.load(f).get(kernel)
-    return None if rec is None else round(rec["hbm_bytes"])
+    for fn in reversed(files):
+        with open(fn) as f:
+            rec = json.load(f).get(kernel)
+        if rec is not None:
+            out = {"hbm_bytes": round(rec["hbm_bytes"]), "source": os.path.basename(fn)}
+            if "mfma_busy" in rec:
+                out["mfma_busy"] = round(rec["mfma_busy"], 4)
+            return out
+    return {}
 
 
 def cpu_baseline(S: int, D: int, H: int):

@@ -105,7 +105,9 @@ struct Scratch {
   std::map<ScratchKey, std::pair<void*, size_t>> bufs;
 } g_scratch;
 
-mfa_status_t scratch(size_t bytes, void** out, int slot, hipStream_t stream) {
+// zero_bytes: the first bytes of a newly allocated buffer are zeroed (stream-ordered), e.g.
+// arrival counters that every launch leaves at zero.
+mfa_status_t scratch(size_t bytes, void** out, int slot, hipStream_t stream, size_t zero_bytes = 0) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(MFA_ERR_NO_DEVICE, "no HIP device");
   std::lock_guard<std::mutex> lock(g_scratch.mu);
@@ -116,6 +118,10 @@ mfa_status_t scratch(size_t bytes, void** out, int slot, hipStream_t stream) {
     void* p = nullptr;
     hipError_t e = hipMallocAsync(&p, bytes, stream);
     if (e != hipSuccess) return hip_status(e, "hipMallocAsync(scratch)");
+    if (zero_bytes && (e = hipMemsetAsync(p, 0, zero_bytes, stream)) != hipSuccess) {
+      (void)hipFreeAsync(p, stream);
+      return hip_status(e, "hipMemsetAsync(scratch)");
+    }
     b = {p, bytes};
   }
   *out = b.first;
@@ -287,6 +293,19 @@ hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, 
     if (e[0] == '1') return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
   }
   if (fwd2_eligible(p, elem, DP, kvsrc)) {
+    // Causal shapes with enough work take the stream-split kernel, which needs a workspace
+    // (arrival counters + partial states, library scratch slot 10).
+    size_t zb = 0;
+    const size_t wsb = mfa::fwd_stream_workspace_bytes(p, elem, DP, &zb);
+    if (wsb) {
+      mfa::FwdParams q = p;
+      if (mfa::plan_capture()) q.ws = (void*)kPlanDummy;
+      else if (scratch(wsb, &q.ws, 10, s, zb) != MFA_SUCCESS) q.ws = nullptr;
+      if (q.ws) {
+        hipError_t e = mfa::fwd_stream_dispatch(q, elem, DP, s);
+        if (e != hipErrorNotSupported) return e;
+      }
+    }
     hipError_t e = mfa::fwd2_dispatch(p, elem, DP, s);
     if (e != hipErrorNotSupported) return e;
   }

@@ -43,6 +43,12 @@ struct FwdParams {
   float c_log2;            // softmax_scale * log2(e) * folded quant scales of Q and K
   float o_mul;             // folded quant scale of V
   MaskArgs mask;
+  // Stream-split causal forward (attention_fwd_stream.hip): workspace = arrival counters
+  // (sk_cnt_bytes, zero between launches) then two partial-state slots per range; ranges of
+  // sk_len key tiles over sk_total tiles (sk_head per (batch, head)).
+  void* ws;
+  int32_t sk_len, sk_total, sk_head, sk_cnt_bytes;
+  int32_t sk_flags;        // bit 0: closers always publish (tests)
 };
 
 struct BwdParams {

@@ -31,6 +31,14 @@ __device__ __forceinline__ int8_t ld_i4(const uint8_t* base, int64_t e) {
   return (int8_t)(nib - 8);
 }
 
+// Row of the 2-D [rows, cols] quantisation view holding row `row` of head (b, hx).  Quantised
+// operands are dense (row-major or transposed within each head, make_operand), so head (b, hx)
+// starts at view row (b·sb + hx·sh) / cols whatever the layout inside the head; the element
+// offset divided by cols would give the wrong row for a transposed head (ss = 1).
+__device__ __forceinline__ int64_t quant_row(const Operand& op, int b, int hx, int64_t row) {
+  return ((int64_t)b * op.sb + (int64_t)hx * op.sh) / op.cols + row;
+}
+
 // Dequantised value of quantised element (row2d, col) with integer payload qv.
 __device__ __forceinline__ float dequant(const Operand& op, int qv, int64_t row2d, int col) {
   if (op.bscale) {
@@ -184,6 +192,7 @@ struct Stager {
       const int grow = row0 + r;
       const int d0 = c * CE;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      uint4 v2 = make_uint4(0u, 0u, 0u, 0u);  // upper half of an FP32-stored chunk
       if ((NCH % NT == 0 || id < NCH) && grow < nrows && d0 < D) {
         const int64_t rowoff =
             (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss + coff;
@@ -195,13 +204,13 @@ struct Stager {
             const float* base = (const float*)op.ptr + rowoff;
             if (op.vec && d0 + 8 <= D) {
               v = *reinterpret_cast<const uint4*>(base + d0);
-              raw2[i] = *reinterpret_cast<const uint4*>(base + d0 + 4);
+              v2 = *reinterpret_cast<const uint4*>(base + d0 + 4);
             } else {
               auto e = [&](int j) -> uint32_t {
                 return d0 + j < D ? __builtin_bit_cast(uint32_t, base[(int64_t)(d0 + j) * op.sd]) : 0u;
               };
               v = make_uint4(e(0), e(1), e(2), e(3));
-              raw2[i] = make_uint4(e(4), e(5), e(6), e(7));
+              v2 = make_uint4(e(4), e(5), e(6), e(7));
             }
           } else {
             const uint16_t* p = (const uint16_t*)op.ptr + rowoff;
@@ -226,10 +235,10 @@ struct Stager {
           v = load_qchunk<SRC>(op, rowoff, d0, D);
         }
       }
+      // One unconditional assignment per register array (assignments in the branches above
+      // made hipcc keep raw2 in scratch).
       raw[i] = v;
-      if constexpr (SRC == SRC_F32ANY) {
-        if (!((NCH % NT == 0 || id < NCH) && grow < nrows && d0 < D)) raw2[i] = make_uint4(0u, 0u, 0u, 0u);
-      }
+      if constexpr (SRC == SRC_F32ANY) raw2[i] = v2;
     }
   }
 
@@ -268,10 +277,7 @@ struct Stager {
           // Per-tensor: the exact integers (q - zp); zero-filled loads beyond the tile edge
           // only ever meet zero Q columns or masked keys.
           const int grow = row0 + r;
-          const int64_t row2d =
-              op.bscale
-                  ? ((int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)grow * op.ss) / op.cols
-                  : 0;
+          const int64_t row2d = op.bscale ? quant_row(op, b, hx, grow) : 0;
           out = convert_qchunk<typename A::Elem, SRC>(raw[i], op, row2d, c * 8, D, grow < nrows);
         }
         *reinterpret_cast<uint4*>(tile + A::TileT::off(r, c)) = out;
@@ -295,7 +301,7 @@ __device__ __forceinline__ void load_row_frags(typename A::frag (&f)[A::DSTEPS],
       f[s] = (valid && d < D) ? base[(int64_t)d * op.sd] : 0.f;
     }
   } else {
-    const int64_t row2d = (op.prec == P_INT8 || op.prec == P_INT4) ? rowoff / op.cols : 0;
+    const int64_t row2d = (op.prec == P_INT8 || op.prec == P_INT4) ? quant_row(op, b, hx, row) : 0;
 #pragma unroll
     for (int s = 0; s < A::DSTEPS; ++s) {
       const int d0 = 16 * s + 8 * h;

@@ -31,6 +31,16 @@ def test_c2_headline_runs_shared_tile_pair_kernel():
     assert p["workgroups"] == 16 * 16
 
 
+def test_large_causal_runs_stream_split_kernel():
+    # Past the mirrored kernel's range (2048 128-row blocks): the key tiles of all heads are
+    # cut into one equal range per CU (256 when no GPU is visible to ask).
+    p = one(mfa.multihead_plan(mh(4, 16, 4096, 128, causal=True)))
+    assert p["name"] == "mfa_fwd2_stream_kernel<F16, 128, 64>"
+    # Two-slot ring of 64-key K/V tiles, one O row image of 128 rows above it, decision word.
+    assert p["threads"] == 512 and p["lds_bytes"] == 4 * 64 * 128 * 2 + 128 * (128 * 4 + 16) + 16
+    assert p["workgroups"] == 256
+
+
 def test_c3_runs_adjacent_shared_tile_kernel():
     # Unmasked with >= 256 block pairs: adjacent 128-row blocks share every K/V tile.
     p = one(mfa.multihead_plan(mh(1, 16, 8192, 128)))

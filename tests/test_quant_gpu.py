@@ -604,3 +604,62 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, monkeypatch):
         assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
     else:
         assert maxerr(o1, o2) < 1e-5 and maxerr(l1, l2) < 2e-2
+
+
+@pytest.mark.parametrize("blockwise", [None, 16])
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+def test_transposed_quantized_kv_matches_row_major(gpu, blockwise, kv):
+    # A transposed K / V (column-major within each head, AttentionKernelDescriptor
+    # transposeState) changes where the bytes sit, not which block scale an element uses: the
+    # blockwise view is the logical [B·Hkv·S, D] one (the scale row was taken from
+    # the element offset, which reads row 0's scales for every row s < D of a transposed head).
+    # Same quantised values and scales in both layouts: both outputs match attention on the
+    # dequantised values (the two layouts may run different kernels, so not bit for bit).
+    B, H, S, D = 1, 2, 96, 64
+    rng = np.random.default_rng(21)
+    Q, K, V = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
+    # Column scale ramps make a wrong scale row visible.
+    K *= np.linspace(0.2, 3.0, S, dtype=np.float32)[None, None, :, None]
+    V *= np.linspace(3.0, 0.2, S, dtype=np.float32)[None, None, :, None]
+    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    keep, deq = [], []
+
+    def qt(x, transposed):
+        rows, cols = x.size // D, D
+        if blockwise:
+            sc = ol.quant_scales_block(x, rows, cols, blockwise, int(kv))
+            q = ol.quantize_block(x, cols, blockwise, int(kv), sc)
+            kw = {"block_scales": tdev(sc), "block_size": blockwise}
+            if not transposed:
+                deq.append(ol.dequantize_block(q, x.size, cols, blockwise, int(kv), sc).reshape(x.shape))
+        else:
+            s = ol.quant_scale_tensor(x, int(kv))
+            q = ol.quantize(x, int(kv), s)
+            kw = {"scale": s}
+            if not transposed:
+                deq.append(ol.dequantize(q, x.size, int(kv), s).reshape(x.shape))
+        if kv == P.INT4:  # unpack nibbles (element 2i low) to permute them, then repack
+            e = np.empty(x.size, np.uint8)
+            e[0::2], e[1::2] = q[: (x.size + 1) // 2] & 15, q[: x.size // 2] >> 4
+        else:
+            e = np.asarray(q, np.uint8)[: x.size]
+        if transposed:
+            e = np.ascontiguousarray(e.reshape(B, H, S, D).transpose(0, 1, 3, 2)).ravel()
+        if kv == P.INT4:
+            e = (e[0::2] | (e[1::2] << 4)).astype(np.uint8)
+        t = mfa.quantized_tensor(tdev(e, torch.uint8), kv, **kw)
+        keep.append(t)
+        return t
+
+    outs = []
+    for tr in (False, True):
+        base = mfa.AttentionDescriptor.make(S, S, D, transpose=(False, tr, tr, False))
+        desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H, Hkv=H)
+        o = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
+        mfa.QuantizedAttention().forward(desc, tq, qt(K, tr), qt(V, tr), o)
+        torch.cuda.synchronize()
+        outs.append(o)
+    ref = ol.attention(seen(Q, P.FP16), deq[0], deq[1])["O"]
+    for o in outs:
+        assert torch.isfinite(o).all()
+        assert maxerr(o, ref) < 5e-3
