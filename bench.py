@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-sparse", action="store_true", help="skip the block-sparse row")
     ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8(f) rows")
     ap.add_argument("--c5-batch", type=int, default=8)
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the heads-split (strong-scaling) C2 row")
     ap.add_argument("--fake-device", action="store_true",
                     help="CPU dry run of the launch / rank / timing plumbing (gloo, no GPU, "
                          "no kernels); used by the CPU test of the --gpus spawn path")
@@ -440,6 +442,35 @@ def main():
         del hx
         result["next_rows"] = nxt
 
+    # ------------------------------------------------- strong scaling: C2 split by heads
+    # SURVEY §8e's plan for C2 / C3 / C4 (B = 1, H = 16): the heads of ONE batch element split
+    # over the N ranks (mfa_shard.forward_slices, no collective).  Reported beside the weak
+    # headline: whole-job TFLOP/s of the one C2 problem, per rank, and the per-GPU occupancy
+    # against this run's weak per-GPU rate (a rank with H/N heads has 1/N of the blocks).
+    if not args.no_strong:
+        mine = shard.forward_slices(1, H, H, world, rank)
+        nh = sum(h1 - h0 for _, h0, h1 in mine)
+        qs, ks, vs = (uniform((1, nh, S, D), torch.float16) for _ in range(3))
+        os_ = torch.empty((1, nh, S, D), dtype=torch.float32, device=dev)
+        ls = torch.empty((1, nh, S), dtype=torch.float16, device=dev)
+        bs = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16,
+                                          causal=True)
+        ds = mfa.MultiHeadDescriptor.make(bs, 1, nh, S, D)
+        fn_s = lambda: mha.forward(ds, qs, ks, vs, os_, ls, stream=stream)
+        warm(fn_s)
+        ns = max(20, args.steps)
+        el_s = timed_steps(fn_s, ns)
+        f_all = mfa.attention_flops(1, H, S, S, D, causal=True)
+        result["strong_heads"] = {
+            "workload": f"C2 (B1 H{H} S{S} D{D} causal fp16) split by heads over {world} rank(s)",
+            "heads_per_rank": nh if world == 1 else f"{H // world}-{-(-H // world)}",
+            "scaling": "strong",
+            "tflops": round(f_all * ns / el_s / 1e12, 2),
+            "tflops_per_rank": round(f_all * ns / el_s / 1e12 / world, 2),
+            "ms_per_step": round(el_s / ns * 1e3, 4),
+            "kernel": mfa.multihead_plan(ds)[0]["name"]}
+        del qs, ks, vs, os_, ls
+
     # ---------------------------------------------------------------- headline: C2
     # Measured last: the sections above have brought the chip to its steady clock (a cold
     # start reads 10-15 % low for the first ~0.1 s of back-to-back launches).
@@ -484,6 +515,11 @@ def main():
     assert len(plan) == 1 and ran and all(r == plan[0] for r in ran), (plan, ran)
     kname = plan[0]["name"]
     pmc = pmc_record(kname, S, H, D)
+    if "strong_heads" in result:
+        # Per-GPU occupancy of the heads split: its per-rank rate over this run's weak per-GPU
+        # rate (1.0 at N = 1 up to timing noise).
+        result["strong_heads"]["per_rank_vs_weak"] = round(
+            result["strong_heads"]["tflops_per_rank"] / (value / world), 4)
     result = {
         "metric": "attn TFLOPS/GPU (fwd seq=4096 d=128) fp16 vs INT8; % MFMA roofline",
         "value": round(value, 2),

@@ -10,7 +10,9 @@ Units:
     [j·H_kv, (j+1)·H_kv).  With the reference's GQA mapping kv = h % H_kv
     (AttentionKernel+Source.swift:96-117) every block reads all H_kv key/value heads in
     order, so a contiguous run of blocks is a dense [B', H', S, D] view of Q/O/L with the same
-    K/V — one launch per batch segment.
+    K/V — one launch per batch segment.  MHA (H_kv == H) splits by single heads: a head range
+    [h0, h1) reads the kv heads [h0, h1), so K/V are sliced with it (strong scaling of one
+    batch element over heads, SURVEY.md §8e's C2/C3/C4 plan).
   * backward: dK/dV are sums over a kv group's query heads, which must stay on one rank:
     MHA (H_kv == H) shards by (b, h); GQA/MQA shards by whole batch elements.
 """
@@ -32,14 +34,15 @@ def forward_slices(B: int, H: int, Hkv: int, world: int, rank: int) -> List[Tupl
     """This rank's forward work as (b, h0, h1) query-head ranges, one per batch segment."""
     if H % Hkv:
         raise ValueError("H must be a multiple of H_kv")
-    blocks = H // Hkv
+    unit = 1 if Hkv == H else Hkv  # heads per unit
+    blocks = H // unit
     u0, u1 = split_range(B * blocks, world, rank)
     out = []
     u = u0
     while u < u1:
         b, j = divmod(u, blocks)
         j1 = min(blocks, j + (u1 - u))
-        out.append((b, j * Hkv, j1 * Hkv))
+        out.append((b, j * unit, j1 * unit))
         u += j1 - j
     return out
 
@@ -62,9 +65,10 @@ def forward_shard(mfa, base, q, k, v, o, l, world: int, rank: int, stream=None) 
     mha = mfa.MultiHeadAttention()
     n = 0
     for b, h0, h1 in forward_slices(B, H, Hkv, world, rank):
-        desc = mfa.MultiHeadDescriptor.make(base, 1, h1 - h0, R, D, Hkv=Hkv, C=C)
-        mha.forward(desc, q[b:b + 1, h0:h1], k[b:b + 1], v[b:b + 1], o[b:b + 1, h0:h1],
-                    None if l is None else l[b:b + 1, h0:h1], stream=stream)
+        hk0, hk1 = (h0, h1) if Hkv == H else (0, Hkv)
+        desc = mfa.MultiHeadDescriptor.make(base, 1, h1 - h0, R, D, Hkv=hk1 - hk0, C=C)
+        mha.forward(desc, q[b:b + 1, h0:h1], k[b:b + 1, hk0:hk1], v[b:b + 1, hk0:hk1],
+                    o[b:b + 1, h0:h1], None if l is None else l[b:b + 1, h0:h1], stream=stream)
         n += h1 - h0
     return n
 

@@ -24,12 +24,26 @@ def test_forward_slices_cover_every_head_once(B, H, Hkv, world):
     for r in range(world):
         n = 0
         for b, h0, h1 in sh.forward_slices(B, H, Hkv, world, r):
-            assert h0 % Hkv == 0 and h1 % Hkv == 0 and h0 < h1  # kv = h % Hkv preserved
+            # kv = h % Hkv preserved: MHA slices K/V with the heads, GQA keeps whole blocks
+            assert Hkv == H or (h0 % Hkv == 0 and h1 % Hkv == 0)
+            assert h0 < h1
             seen[b, h0:h1] += 1
             n += h1 - h0
         sizes.append(n)
     assert (seen == 1).all()
-    assert max(sizes) - min(sizes) <= Hkv  # balanced to one unit
+    unit = 1 if Hkv == H else Hkv
+    assert max(sizes) - min(sizes) <= unit  # balanced to one unit
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8, 16])
+def test_head_split_of_one_batch_element(world):
+    # SURVEY §8e strong-scaling plan: C2 / C3 / C4 (B = 1, H = 16) split over N ranks by heads;
+    # each rank gets ceil or floor of 16 / N heads and the union covers every head once.
+    got = [sh.forward_slices(1, 16, 16, world, r) for r in range(world)]
+    counts = [sum(h1 - h0 for _, h0, h1 in g) for g in got]
+    assert sorted(set(counts)) in ([16 // world], [16 // world, -(-16 // world)])
+    heads = sorted(h for g in got for _, h0, h1 in g for h in range(h0, h1))
+    assert heads == list(range(16))
 
 
 @pytest.mark.parametrize("B,H,Hkv,world", [(2, 8, 8, 3), (3, 8, 2, 2), (4, 4, 1, 4)])
@@ -68,7 +82,8 @@ def _worker(rank, world, port, B, H, Hkv, S, D, q):
     dist.barrier()
     pieces = []
     for b, h0, h1 in sh.forward_slices(B, H, Hkv, world, rank):
-        r = ol.attention(Q[b:b + 1, h0:h1], K[b:b + 1], V[b:b + 1], causal=True)
+        hk0, hk1 = (h0, h1) if Hkv == H else (0, Hkv)
+        r = ol.attention(Q[b:b + 1, h0:h1], K[b:b + 1, hk0:hk1], V[b:b + 1, hk0:hk1], causal=True)
         pieces.append((b, h0, h1, r["O"], r["L"]))
     dist.barrier()
     t = torch.tensor([1.0 + rank])
@@ -87,7 +102,7 @@ def _worker(rank, world, port, B, H, Hkv, S, D, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B,H,Hkv", [(2, 4, 4), (3, 4, 2)])
+@pytest.mark.parametrize("B,H,Hkv", [(2, 4, 4), (3, 4, 2), (1, 4, 4)])
 def test_gloo_world2_sharded_forward_equals_unsharded(B, H, Hkv):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
