@@ -236,11 +236,30 @@ def main():
                 "kernels": [r["name"] for r in mfa.quantized_plan(qdd, mfa.KernelType.forward,
                                                                    tqd, tkd, tvd)],
             }
+            if Rd == 1:
+                # The same cache as INT4 (two elements per byte): half the K/V bytes.
+                kd4 = kd8[..., : Dd // 2].contiguous()
+                vd4 = vd8[..., : Dd // 2].contiguous()
+                tk4 = mfa.quantized_tensor(kd4, mfa.Precision.INT4, scale=0.25 / 7)
+                tv4 = mfa.quantized_tensor(vd4, mfa.Precision.INT4, scale=0.25 / 7)
+                qd4 = mfa.quantized_descriptor(based, mfa.Precision.FP16, mfa.Precision.INT4,
+                                               mfa.Precision.INT4, B=Bd, H=Hd)
+                ms4 = ev_time(lambda: qa.forward(qd4, tqd, tk4, tv4, od8, ld8, stream=stream))
+                io4 = kv_bytes // 2 + qd8.numel() * 2 + od8.numel() * 4 + ld8.numel() * 2
+                dec["s_q1_int4"] = {
+                    "ms": round(ms4, 4),
+                    "GBps": round(io4 / ms4 / 1e6, 1),
+                    "hbm_frac": round(io4 / ms4 / 1e6 / 8000.0, 4),
+                    "kernels": [r["name"] for r in mfa.quantized_plan(qd4, mfa.KernelType.forward,
+                                                                       tqd, tk4, tv4)],
+                }
+                del kd4, vd4
             del qd8, od8, ld8
         result["int8_decode"] = {
             "workload": f"QuantizedAttention forward, INT8 K/V (per-tensor) + fp16 Q, B{Bd} H{Hd} "
-                        f"S_kv {Cd} D{Dd}, S_q 1 and 16 (decode / KV cache), non-causal",
-            "bytes": "INT8 K + V once, plus Q (fp16), O (fp32) and L (fp16); roof 8 TB/s HBM",
+                        f"S_kv {Cd} D{Dd}, S_q 1 and 16 (decode / KV cache), non-causal; "
+                        f"s_q1_int4: the same shape with INT4 K/V",
+            "bytes": "INT8 (INT4) K + V once, plus Q (fp16), O (fp32) and L (fp16); roof 8 TB/s HBM",
             **dec,
         }
         del kd8, vd8

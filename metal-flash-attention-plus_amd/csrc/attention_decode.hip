@@ -70,22 +70,32 @@ __device__ __forceinline__ void merge_partials(const FwdParams& p, const float2*
   }
 }
 
-template <class E, int DP>
+// SRC_I8: one byte per element.  SRC_I4: two per byte (element 2i in the low nibble,
+// GEMMQuantization.swift:500-515); the packed tile is staged by LDS-DMA as stored and widened
+// in LDS to the INT8 tile layout (nibble n as the byte n, the zero point raised by 8: the
+// nibble encodes n - 8), after which both paths run the same INT8 loop.
+template <class E, int DP, int SRC = SRC_I8>
 __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(DecodeParams dp) {
   const FwdParams& p = dp.f;
+  constexpr bool I4 = SRC == SRC_I4;
   constexpr int BK = 32, NSLOT = 2, ND = DP / 32;
-  constexpr int ROWB = DP;                  // INT8: one byte per element
+  constexpr int ROWB = DP;                  // INT8 compute tile: one byte per element
   using T = Tile16<ROWB / 2>;               // [BK][ROWB bytes], 16-byte chunks XOR-swizzled
-  constexpr int TILEB = BK * ROWB;          // one K or V tile
-  constexpr int NPC = TILEB / 1024;         // 1-KiB DMA pieces per tile
-  constexpr int RP = 1024 / ROWB;           // rows per piece
+  constexpr int TILEB = BK * ROWB;          // one K or V compute tile
+  constexpr int ROWBS = I4 ? DP / 2 : DP;   // bytes per stored row
+  constexpr int TILEBS = BK * ROWBS;        // one stored (DMA) tile
+  constexpr int NPC = TILEBS / 1024;        // 1-KiB DMA pieces per tile
+  constexpr int RP = 1024 / ROWBS;          // rows per piece
   static_assert(NPC >= 1 && NPC <= 8, "decode tile geometry");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  char* const ring = smem + wave * (NSLOT * 2 * TILEB);  // slot s: K at 2s·TILEB, V after it
+  // Per wave: NSLOT DMA slots (K at 2s·TILEBS, V after it); INT4 also one widened INT8 K and V
+  // tile after them (4·TILEB in all for INT8, 3·TILEB for INT4).
+  char* const ring = smem + wave * (NSLOT * 2 * TILEB);
+  char* const conv = ring + NSLOT * 2 * TILEBS;
 
   const int split = blockIdx.x;
   const int u = blockIdx.y + gridDim.y * blockIdx.z;    // (b·H_kv + kvh)·nrt + rt
@@ -122,31 +132,60 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   // contiguous); lane l lands at byte 16·l of it = row n·RP + l / CPR, physical chunk l % CPR,
   // so it fetches logical chunk (l % CPR) ^ swz(row).  Rows past C and chunks past D read as
   // zeros (range-checked descriptor per piece, out-of-row chunks out of range).
-  constexpr int CPR = ROWB / 16;
+  // (INT4: the packed rows land unswizzled, as stored; the widening writes the swizzled INT8
+  // layout.)
+  constexpr int CPR = ROWBS / 16;
+  constexpr int SH = I4 ? 1 : 0;  // element -> byte offsets
+  const int ssb = (int)(p.k.ss >> SH);
   int poff[NPC];
 #pragma unroll
   for (int n = 0; n < NPC; ++n) {
     const int r = n * RP + lane / CPR;
-    const int ch = (lane % CPR) ^ T::swz(r);
-    poff[n] = ch * 16 < p.D ? r * (int)p.k.ss + ch * 16 : 0x40000000;
+    const int ch = I4 ? lane % CPR : (lane % CPR) ^ T::swz(r);
+    poff[n] = ch * 16 < (p.D >> SH) ? r * ssb + ch * 16 : 0x40000000;
   }
-  const char* khead = (const char*)p.k.ptr + (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
-  const char* vhead = (const char*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
-  const int kbytes = (int)((int64_t)(p.C - 1) * p.k.ss + p.D);
-  const int vbytes = (int)((int64_t)(p.C - 1) * p.v.ss + p.D);
+  const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> SH);
+  const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> SH);
+  const int kbytes = (int)((int64_t)(p.C - 1) * ssb + (p.D >> SH));
+  const int vbytes = (int)((int64_t)(p.C - 1) * (p.v.ss >> SH) + (p.D >> SH));
   auto issue = [&](int i, int slot) {
     const int t = k0 + BK * (wave + 4 * i);
-    char* kdst = ring + slot * 2 * TILEB;
+    char* kdst = ring + slot * 2 * TILEBS;
 #pragma unroll
     for (int n = 0; n < NPC; ++n) {
-      const int rk = t * (int)p.k.ss;
+      const int rk = t * ssb;
       lds_dma16(khead + rk, max(kbytes - rk, 0), poff[n], kdst + n * 1024);
     }
 #pragma unroll
     for (int n = 0; n < NPC; ++n) {
-      const int rv = t * (int)p.v.ss;
+      const int rv = t * ssb;
       // V rows share the K piece geometry when the row strides agree (host-checked).
-      lds_dma16(vhead + rv, max(vbytes - rv, 0), poff[n], kdst + TILEB + n * 1024);
+      lds_dma16(vhead + rv, max(vbytes - rv, 0), poff[n], kdst + TILEBS + n * 1024);
+    }
+  };
+  // INT4: the packed tile of this slot widened into the INT8 compute tiles (wave-private: the
+  // wave's own LDS accesses stay in order, no barrier).  Nibbles n0..n3 of a 16-bit half-word
+  // become the bytes n0..n3 by two shift-or-mask steps.
+  auto widen_i4_tile = [&](int slot) {
+    constexpr int NCP = ROWBS / 16, PER = BK * NCP / 64;
+    auto expand = [](uint32_t x) -> uint32_t {
+      x &= 0xFFFFu;
+      x = (x | (x << 8)) & 0x00FF00FFu;
+      return (x | (x << 4)) & 0x0F0F0F0Fu;
+    };
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      const char* src = ring + slot * 2 * TILEBS + op * TILEBS;
+      char* dst = conv + op * TILEB;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int idx = lane + 64 * j, r = idx / NCP, pc = idx % NCP;
+        const uint4 w = *reinterpret_cast<const uint4*>(src + r * ROWBS + pc * 16);
+        *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc)) =
+            make_uint4(expand(w.x), expand(w.x >> 16), expand(w.y), expand(w.y >> 16));
+        *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc + 1)) =
+            make_uint4(expand(w.z), expand(w.z >> 16), expand(w.w), expand(w.w >> 16));
+      }
     }
   };
 
@@ -155,7 +194,7 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   const int trj = (lane & 15) >> 1;
   const int trg = (lane >> 4) & 1;
   const int trow0 = acc_row(trj, hh), trow1 = acc_row(trj + 8, hh);
-  const float zk = (float)p.k.zp, zv = (float)p.v.zp;
+  const float zk = (float)(p.k.zp + (I4 ? 8 : 0)), zv = (float)(p.v.zp + (I4 ? 8 : 0));
 
   f32x16 o[ND];
 #pragma unroll
@@ -172,6 +211,10 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
       wait_vm();
     }
     const char* kt = ring + slot * 2 * TILEB;
+    if constexpr (I4) {
+      widen_i4_tile(slot);
+      kt = conv;
+    }
     const char* vt = kt + TILEB;
     const int t = k0 + BK * (wave + 4 * i);
 
@@ -310,34 +353,46 @@ void decode_layout(int B, int Hkv, int rows, int C, int* nrt, int* nsplit, int* 
   *nsplit = (C + *chunk - 1) / *chunk;
 }
 
+// Partials workspace of the split path; 0 when a unit's keys fit one split and the workgroup
+// merges its waves' partials in LDS (the kernel then never touches the workspace).
+static bool decode_fused(int nsplit) {
+  const char* mv = getenv("MFA_DECODE_MERGE");  // =1: the separate merge pass for one split too
+  return nsplit == 1 && !(mv && mv[0] == '1');
+}
+
 size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D) {
   int nrt, ns, chunk;
   decode_layout(B, Hkv, rows, C, &nrt, &ns, &chunk);
+  if (decode_fused(ns)) return 0;
   const size_t parts = (size_t)B * Hkv * nrt * ns * 4 * 32;
   return parts * D * 4 + parts * 8 + 256;
 }
 
 hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hipStream_t stream) {
-  if (p.k.prec != P_INT8 || p.v.prec != P_INT8 || p.k.ss != p.v.ss) return hipErrorNotSupported;
+  const bool i4 = p.k.prec == P_INT4;
+  if (p.k.prec != p.v.prec || (p.k.prec != P_INT8 && !i4) || p.k.ss != p.v.ss)
+    return hipErrorNotSupported;
   DecodeParams dp;
   dp.f = p;
   dp.rows = (p.H / p.Hkv) * p.R;
   decode_layout(p.B, p.Hkv, dp.rows, p.C, &dp.nrt, &dp.nsplit, &dp.chunk);
   const size_t parts = (size_t)p.B * p.Hkv * dp.nrt * dp.nsplit * 4 * 32;
   dp.opart = (float*)workspace;
-  dp.mlpart = (float2*)((char*)workspace + ((parts * p.D * 4 + 255) & ~(size_t)255));
+  dp.mlpart = workspace ? (float2*)((char*)workspace + ((parts * p.D * 4 + 255) & ~(size_t)255))
+                        : nullptr;
   const int units = p.B * p.Hkv * dp.nrt;
   if (units >= 65536) return hipErrorNotSupported;
   const dim3 grid(dp.nsplit, units, 1);
   const int DP = p.D <= 64 ? 64 : p.D <= 128 ? 128 : 256;
-  // MFA_DECODE_MERGE=1 keeps the separate merge pass for one split too (A/B, tests).
-  const char* mv = getenv("MFA_DECODE_MERGE");
-  dp.fused = dp.nsplit == 1 && !(mv && mv[0] == '1');
+  dp.fused = decode_fused(dp.nsplit);
+  if (!dp.fused && !workspace) return hipErrorInvalidValue;
   hipError_t e = hipErrorNotSupported;
 #define MFA_DEC(ELEM, EE, DPV)                                                                 \
   if (elem == ELEM && DP == DPV)                                                               \
-    e = launch(mfa_fwd_decode_kernel<EE, DPV>, grid, dim3(256), 4 * 2 * 2 * 32 * DPV + 1024,  \
-               stream, dp);
+    e = i4 ? launch(mfa_fwd_decode_kernel<EE, DPV, SRC_I4>, grid, dim3(256),                   \
+                    4 * 2 * 2 * 32 * DPV + 1024, stream, dp)                                   \
+           : launch(mfa_fwd_decode_kernel<EE, DPV, SRC_I8>, grid, dim3(256),                   \
+                    4 * 2 * 2 * 32 * DPV + 1024, stream, dp);
   MFA_DEC(P_FP16, F16, 64)
   MFA_DEC(P_FP16, F16, 128)
   MFA_DEC(P_FP16, F16, 256)

@@ -41,18 +41,34 @@ __device__ __forceinline__ bool masked_everywhere(const FwdParams& p, uint32_t x
   return lo >= hi;
 }
 
-template <class E>
-__device__ __forceinline__ void fill_masked_row(const FwdParams& p, int b, int h, int kvh, int q,
-                                                int lane) {
+// The wave's empty rows (bit r of `rows`: row q0w + r) all get the same mean of V, so it is
+// summed once per wave (keys in order, lanes across the head dimension) and written to each;
+// a per-row sum made block-sparse patterns with many empty rows cost O(rows·C·D/64).
+template <class E, int DP>
+__device__ __forceinline__ void fill_masked_rows(const FwdParams& p, int b, int h, int kvh, int q0w,
+                                                 uint64_t rows, int lane) {
+  constexpr int NDV = (DP + 63) / 64;
   const uint16_t* vbase = (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
-  float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
   const float l = (float)p.C;
-  for (int d = lane; d < p.D; d += 64) {
-    float acc = 0.f;
-    for (int k = 0; k < p.C; ++k) acc += E::to_f32(vbase[(int64_t)k * p.v.ss + (int64_t)d * p.v.sd]);
-    orow[(int64_t)d * p.o_sd] = acc * (p.o_mul / l);
+  float acc[NDV];
+#pragma unroll
+  for (int j = 0; j < NDV; ++j) {
+    const int d = lane + 64 * j;
+    acc[j] = 0.f;
+    if (d < p.D)
+      for (int k = 0; k < p.C; ++k) acc[j] += E::to_f32(vbase[(int64_t)k * p.v.ss + (int64_t)d * p.v.sd]);
+    acc[j] *= p.o_mul / l;
   }
-  if (lane == 0) store_l(p, mul_rn(kMaskValue, p.c_log2) + __log2f(l), b, h, q);
+  const float L = mul_rn(kMaskValue, p.c_log2) + __log2f(l);
+  while (rows) {
+    const int q = q0w + __builtin_ctzll(rows);
+    rows &= rows - 1;
+    float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
+#pragma unroll
+    for (int j = 0; j < NDV; ++j)
+      if (lane + 64 * j < p.D) orow[(int64_t)(lane + 64 * j) * p.o_sd] = acc[j];
+    if (lane == 0) store_l(p, L, b, h, q);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -93,7 +109,7 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   key_range(p, q0, BQ, BK, &kbeg, &kend);
   // Sparse ranges (SparseMQABuilder, AttentionKernel+Softmax.swift:278-304): the row's keys
   // [x, y); tiles outside the union of the block's non-empty ranges are skipped.  Rows left
-  // with no unmasked key are written by their wave after the loop (fill_masked_row: the
+  // with no unmasked key are written by their wave after the loop (fill_masked_rows: the
   // reference's finite mask value makes them a uniform average over every key).
   int rlo = -0x40000000, rhi = 0x3fffffff;
   int in_lo = 0, in_hi = 0x3fffffff;  // keys inside every non-empty range of the block
@@ -195,13 +211,9 @@ __global__ void __launch_bounds__(256, WPS) mfa_fwd2_kernel(FwdParams p) {
   if (!(l > 0.f)) l = kFltMin;
   if (qvalid && !row_empty) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
   if (p.mask.ranges) {
-    // The wave writes its rows with no unmasked key itself, one row at a time (rare).
-    uint64_t todo = __ballot(row_empty && hh == 0);
-    while (todo) {
-      const int src = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      fill_masked_row<E>(p, b, h, kvh, q0 + wave * 32 + src, lane);
-    }
+    // The wave writes its rows with no unmasked key itself (rare).
+    const uint64_t todo = __ballot(row_empty && hh == 0);
+    if (todo) fill_masked_rows<E, DP>(p, b, h, kvh, q0 + wave * 32, todo, lane);
   }
   MFA_STAMP(3);
   MFA_CYC(1);

@@ -718,23 +718,27 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
          ((uintptr_t)p.v.ptr % 4 == 0);
 }
 
-// The split-KV decode kernel (attention_decode.hip): FP16/BF16 Q, per-tensor INT8 K/V with
-// the same row layout, 16-byte rows, D % 16 == 0, D <= 256, no mask, dense O rows.
+// The split-KV decode kernel (attention_decode.hip): FP16/BF16 Q, per-tensor INT8 or INT4
+// K/V with the same row layout, 16-byte rows (INT4: D % 32 == 0, 16-byte packed rows), D <= 256,
+// no mask, dense O rows.
 bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
   if (const char* e = getenv("MFA_DECODE")) {
     if (e[0] == '0') return false;
   }
   if (elem != 1 && elem != 2) return false;
-  if (is_quantized(qp) || kp != MFA_PRECISION_INT8 || vp != MFA_PRECISION_INT8) return false;
+  if (is_quantized(qp) || kp != vp || (kp != MFA_PRECISION_INT8 && kp != MFA_PRECISION_INT4))
+    return false;
+  const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
   if (p.k.bscale || p.v.bscale) return false;
-  if (p.D % 16 != 0 || p.D > 256 || p.C <= 0 || !(p.c_log2 > 0.f)) return false;
+  if (p.D % (16 << sh) != 0 || p.D > 256 || p.C <= 0 || !(p.c_log2 > 0.f)) return false;
   if (p.mask.causal || p.mask.window || p.mask.amask || p.mask.ranges) return false;
   if (p.q.sd != 1 || !p.q.vec || p.k.sd != 1 || p.v.sd != 1) return false;
-  if (p.k.ss != p.v.ss || p.k.ss % 16 || p.k.sh % 16 || p.k.sb % 16 || p.v.sh % 16 ||
-      p.v.sb % 16)
+  const int64_t al = 16 << sh;
+  if (p.k.ss != p.v.ss || p.k.ss % al || p.k.sh % al || p.k.sb % al || p.v.sh % al ||
+      p.v.sb % al)
     return false;
   if ((uintptr_t)p.k.ptr % 16 || (uintptr_t)p.v.ptr % 16) return false;
-  return (int64_t)p.C * p.k.ss < ((int64_t)1 << 31);
+  return ((int64_t)p.C * p.k.ss >> sh) < ((int64_t)1 << 31);
 }
 
 // The on-load shared-tile forward (attention_fwd_kv8.hip): FP16 Q, per-tensor INT8 or INT4
@@ -757,7 +761,9 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
     if (o->ss % (16 << sh) || o->sh % (16 << sh) || o->sb % (16 << sh) ||
         (uintptr_t)o->ptr % 16)
       return false;
-  return (int64_t)p.C * p.k.ss < ((int64_t)1 << 31) && (int64_t)p.C * p.v.ss < ((int64_t)1 << 31);
+  // Byte offsets are 32-bit, including the prefetch of tile t + 2 (up to 2·64 rows past C).
+  const int64_t rows = (int64_t)p.C + 256;
+  return (rows * p.k.ss >> sh) < ((int64_t)1 << 31) && (rows * p.v.ss >> sh) < ((int64_t)1 << 31);
 }
 
 // Quantised operands go through one dequantisation pass into a dense 16-bit copy
@@ -869,11 +875,13 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
   }
   if (decode_eligible(p, elem, qp, kp, vp) && !dequant_pass_worth(R, H, Hkv, D, elem)) {
     // Decode / KV-cache shapes: split-KV kernel reading the INT8 bytes (attention_decode.hip).
+    // The split-KV partials workspace (scratch slot 9), unless one split per unit merges in
+    // LDS (decode_workspace_bytes returns 0: nothing is allocated).
     void* ws = nullptr;
-    if (mfa::plan_capture()) {
+    const size_t wsb = mfa::decode_workspace_bytes(B, Hkv, (H / Hkv) * R, C, D);
+    if (wsb && mfa::plan_capture()) {
       ws = (void*)kPlanDummy;
-    } else if ((st = scratch(mfa::decode_workspace_bytes(B, Hkv, (H / Hkv) * R, C, D), &ws, 9,
-                             (hipStream_t)stream)) != MFA_SUCCESS) {
+    } else if (wsb && (st = scratch(wsb, &ws, 9, (hipStream_t)stream)) != MFA_SUCCESS) {
       return st;
     }
     const hipError_t e = mfa::fwd_decode_dispatch(p, elem, ws, (hipStream_t)stream);

@@ -66,10 +66,12 @@ inline hipError_t set_lds_attr_per_device(const void* kern, size_t bytes) {
   if (e != hipSuccess) return e;
   LdsAttrTable& t = lds_attr_table();
   std::lock_guard<std::mutex> lock(t.mu);
+  // Only successful sets are remembered (the largest size set so far): a failed request is
+  // retried by the next launch instead of failing every later one of that kernel.
   auto it = t.set.find({kern, dev});
-  if (it != t.set.end() && it->second.first >= bytes) return it->second.second;
+  if (it != t.set.end() && it->second.first >= bytes) return hipSuccess;
   e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  t.set[{kern, dev}] = {bytes, e};
+  if (e == hipSuccess) t.set[{kern, dev}] = {bytes, e};
   return e;
 }
 

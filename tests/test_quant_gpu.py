@@ -519,6 +519,61 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
         assert torch.equal(o, o3) and torch.equal(l, l3)
 
 
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,qp", [
+    (2, 4, 4, 1, 1000, 128, P.FP16),
+    (1, 8, 2, 3, 777, 64, P.BF16),     # GQA
+    (2, 4, 1, 5, 300, 256, P.FP16),    # MQA, D 256
+    (1, 16, 1, 4, 300, 128, P.FP16),   # two row tiles, one split: in-workgroup merge
+    (1, 2, 2, 16, 4101, 128, P.BF16),  # 16 query rows, partial last tile
+])
+def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
+    # INT4 K/V cache at decode shapes on the split-KV kernel: the packed tiles are staged as
+    # stored and widened in LDS to the INT8 layout.  Held to the oracle on the dequantised
+    # values and to the generic dequant-on-load kernel (MFA_DECODE=0).
+    rng = np.random.default_rng(R * 17 + C)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, P.INT4, P.INT4, B=B, H=H, Hkv=Hkv)
+    names = [r["name"] for r in mfa.quantized_plan(desc)]
+    assert names[0].startswith("mfa_fwd_decode_kernel<") and names[0].endswith(", 2>"), names
+    o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT4, P.INT4)
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"])
+    assert np.isfinite(o.cpu().numpy()).all()
+    assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
+    assert maxerr(l, ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max()
+    monkeypatch.setenv("MFA_DECODE", "0")
+    o2, _, _, _ = run_qforward(Q, K, V, qp, P.INT4, P.INT4)
+    monkeypatch.delenv("MFA_DECODE")
+    assert maxerr(o, o2.cpu().numpy()) < 2e-3
+
+
+def test_decode_int4_zero_points(gpu):
+    # Per-tensor zero points on INT4 bytes: nibble n is n - 8, minus zp, exactly.
+    B, H, R, C, D = 1, 2, 2, 700, 128
+    rng = np.random.default_rng(6)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    kn = rng.integers(0, 16, (B, H, C, D)).astype(np.uint8)
+    vn = rng.integers(0, 16, (B, H, C, D)).astype(np.uint8)
+    pack = lambda n: (n.reshape(-1)[0::2] | (n.reshape(-1)[1::2] << 4)).astype(np.uint8)
+    ks, vs, kz, vz = 0.2, 0.3, 3, -2
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=P.FP16)
+    desc = mfa.quantized_descriptor(base, P.FP16, P.INT4, P.INT4, B=B, H=H)
+    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    tk = mfa.quantized_tensor(tdev(pack(kn), torch.uint8), P.INT4, scale=ks, zero_point=kz)
+    tv = mfa.quantized_tensor(tdev(pack(vn), torch.uint8), P.INT4, scale=vs, zero_point=vz)
+    o = torch.empty((B, H, R, D), dtype=torch.float32, device=DEV)
+    l = torch.empty((B, H, R), dtype=torch.float16, device=DEV)
+    assert mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)[0]["name"].startswith(
+        "mfa_fwd_decode_kernel<")
+    mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+    torch.cuda.synchronize()
+    Kd = (kn.astype(np.float32) - 8 - kz) * np.float32(ks)
+    Vd = (vn.astype(np.float32) - 8 - vz) * np.float32(vs)
+    ref = ol.attention(seen(Q, P.FP16), Kd, Vd)
+    assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
+
+
 def test_decode_nonzero_zero_point(gpu):
     # Per-tensor zero points ride into the widening as (q - zp), exactly.
     B, H, R, C, D = 1, 2, 2, 500, 128

@@ -102,3 +102,21 @@ def test_ranges_beyond_sequence(gpu):
     Q = gaussian((B, H, R, D), 922)
     K, V = gaussian((B, H, C, D), 923), gaussian((B, H, C, D), 924)
     check(Q, K, V, BF16, ranges)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_mostly_empty_rows(gpu, D):
+    """a pattern whose rows are mostly empty (every block row but one per four has
+    no keys, and single rows emptied in the live ones) over a long key range: the empty rows of
+    a wave share one mean of V, summed once per wave."""
+    B, H, Hkv, R, C, blk = 1, 2, 2, 512, 2048, 64
+    nqb, nkb = R // blk, C // blk
+    pat = np.zeros((nqb, nkb), dtype=np.uint8)
+    pat[::4, : nkb // 2] = 1
+    ranges = np.stack([block_ranges(pat, blk, R, C) for _ in range(Hkv)])[None]
+    ranges[0, 0, 7::9, 1] = ranges[0, 0, 7::9, 0]
+    assert (ranges[..., 0] >= ranges[..., 1]).mean() > 0.7
+    Q = gaussian((B, H, R, D), 930)
+    K, V = gaussian((B, Hkv, C, D), 931), gaussian((B, Hkv, C, D), 932)
+    plan = check(Q, K, V, FP16, ranges)
+    assert len(plan) == 1 and "mfa_fwd2_kernel" in plan[0], plan
