@@ -351,6 +351,28 @@ mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* desc,
                                    const mfa_quantized_tensor_t* value, float* output,
                                    void* logsumexp, const void* mask, void* stream);
 
+/* QuantizedAttention.forward(queryBuffer:keyBuffer:valueBuffer:output:queryShape:keyShape:
+ * valueShape:queryPrecision:keyPrecision:valuePrecision:targetQuantization:quantizationMode:
+ * descriptor:) (QuantizedAttention.swift:278-336; the uniform-settings overload :349-372 is this
+ * call with one precision for all three).  Q, K and V arrive as FP32 / FP16 / BF16 device
+ * tensors ([B, H, R, D], [B, H_kv, C, D], dense, shapes from the descriptor) and are quantized
+ * on the GPU (mfa_quantize) to `target_precision` in `mode` (tensor-wise or blockwise with
+ * `block_size`) into library scratch on `stream`, then run through mfa_quantized_forward with
+ * the configuration's precisions replaced by the target for all three operands (every tensor
+ * handed to that forward is then target-quantized, as in the reference).  A target that needs
+ * no quantization parameters (FP16 / BF16 / FP32) wraps the buffers as they are (:425-441).
+ * Tensor-wise scales are read back to the host before the forward (one synchronisation of
+ * `stream`; the reference computes them on the CPU, :479-498); blockwise scales stay on the
+ * device and the call stays asynchronous.  Row-wise mode is not an attention input layout:
+ * MFA_ERR_UNSUPPORTED. */
+mfa_status_t mfa_quantized_forward_from_float(const mfa_quantized_descriptor_t* desc,
+                                              const void* query, const void* key,
+                                              const void* value, int32_t query_precision,
+                                              int32_t key_precision, int32_t value_precision,
+                                              int32_t target_precision, int32_t mode,
+                                              uint32_t block_size, float* output,
+                                              void* logsumexp, const void* mask, void* stream);
+
 /* QuantizedAttention.backwardQuery (:1012-1097) and backwardKeyValue (:1102-1181).
  * dO/L/D/O use the base descriptor's memory precisions (FP32 unless low precision). */
 mfa_status_t mfa_quantized_backward_query(const mfa_quantized_descriptor_t* desc,

@@ -905,6 +905,89 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
                     "mfa_fwd (quantized) launch");
 }
 
+// Runtime-quantising forward (QuantizedAttention.swift:278-372): quantize Q, K, V on the GPU,
+// then the quantized forward.
+extern "C" mfa_status_t mfa_quantized_forward_from_float(
+    const mfa_quantized_descriptor_t* desc, const void* query, const void* key, const void* value,
+    int32_t query_precision, int32_t key_precision, int32_t value_precision,
+    int32_t target_precision, int32_t mode, uint32_t block_size, float* output, void* logsumexp,
+    const void* mask, void* stream) {
+  if (!desc) return fail(MFA_ERR_INVALID_ARGUMENT, "null argument");
+  const mfa_attention_descriptor_t& base = desc->base;
+  if (!base.has_matrix_dimensions) return fail(MFA_ERR_INVALID_DESCRIPTOR, "Descriptor was incomplete.");
+  const int precs[3] = {query_precision, key_precision, value_precision};
+  for (int p : precs)
+    if (p != MFA_PRECISION_FP32 && p != MFA_PRECISION_FP16 && p != MFA_PRECISION_BF16)
+      return fail(MFA_ERR_UNSUPPORTED, "runtime quantization input precision %d", p);
+  mfa_quantized_descriptor_t d = *desc;
+  mfa_quantized_tensor_t t[3];
+  memset(t, 0, sizeof(t));
+  const void* in[3] = {query, key, value};
+  if (!is_quantized(target_precision)) {
+    // No quantization parameters needed: the buffers as they are (:425-441).
+    d.config.query_precision = query_precision;
+    d.config.key_precision = key_precision;
+    d.config.value_precision = value_precision;
+    for (int i = 0; i < 3; ++i) {
+      t[i].data = in[i];
+      t[i].precision = precs[i];
+      t[i].scale = 1.f;
+    }
+    return mfa_quantized_forward(&d, &t[0], &t[1], &t[2], output, logsumexp, mask, stream);
+  }
+  if (mode != MFA_QUANT_TENSOR_WISE && mode != MFA_QUANT_BLOCKWISE)
+    return fail(MFA_ERR_UNSUPPORTED, "runtime quantization mode %d for attention", mode);
+  if (mode == MFA_QUANT_BLOCKWISE && block_size == 0)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "blockwise quantization with block size 0");
+  const int B = desc->batch_size ? (int)desc->batch_size : 1;
+  const int H = desc->num_heads ? (int)desc->num_heads : 1;
+  const int Hkv = desc->num_kv_heads ? (int)desc->num_kv_heads : H;
+  const uint64_t R = base.row, C = base.column, D = base.head;
+  if (R == 0) return MFA_SUCCESS;
+  if (!query || !key || !value || !output)
+    return fail(MFA_ERR_INVALID_ARGUMENT, "null Q / K / V / output");
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t rows[3] = {(uint64_t)B * H * R, (uint64_t)B * Hkv * C, (uint64_t)B * Hkv * C};
+  float host_scale[3] = {1.f, 1.f, 1.f};
+  float* dev_scale[3] = {nullptr, nullptr, nullptr};
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  for (int i = 0; i < 3; ++i) {
+    const uint64_t count = rows[i] * D;
+    const size_t qb = al(target_precision == MFA_PRECISION_INT8 ? count : (count + 1) / 2);
+    const uint64_t nb = mode == MFA_QUANT_BLOCKWISE
+                            ? ((rows[i] + block_size - 1) / block_size) * ((D + block_size - 1) / block_size)
+                            : 0;
+    const size_t ws = al(mfa_quantize_workspace_size(count, (uint32_t)rows[i], (uint32_t)D, mode, block_size));
+    const size_t bytes = qb + 256 + ws + 2 * al(nb * 4);
+    void* buf = nullptr;
+    if (mfa::plan_capture()) return fail(MFA_ERR_UNSUPPORTED, "plan query of the runtime-quantising forward");
+    mfa_status_t st = scratch(bytes, &buf, 11 + i, s);
+    if (st != MFA_SUCCESS) return st;
+    char* c = (char*)buf;
+    dev_scale[i] = (float*)(c + qb);
+    void* work = c + qb + 256;
+    float* bsc = nb ? (float*)(c + qb + 256 + ws) : nullptr;
+    int32_t* bzp = nb ? (int32_t*)(c + qb + 256 + ws + al(nb * 4)) : nullptr;
+    st = mfa_quantize(in[i], precs[i], count, (uint32_t)rows[i], (uint32_t)D, target_precision, mode,
+                      block_size, c, dev_scale[i], bsc, bzp, ws ? work : nullptr, stream);
+    if (st != MFA_SUCCESS) return st;
+    t[i].data = c;
+    t[i].precision = target_precision;
+    t[i].block_scales = bsc;
+    t[i].block_zero_points = bzp;
+    t[i].block_size = nb ? block_size : 0;
+  }
+  if (mode == MFA_QUANT_TENSOR_WISE) {
+    for (int i = 0; i < 3; ++i)
+      if (hipMemcpyAsync(&host_scale[i], dev_scale[i], 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return fail(MFA_ERR_LAUNCH, "reading back the tensor-wise scales");
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(MFA_ERR_LAUNCH, "stream synchronisation");
+    for (int i = 0; i < 3; ++i) t[i].scale = host_scale[i];
+  }
+  d.config.query_precision = d.config.key_precision = d.config.value_precision = target_precision;
+  return mfa_quantized_forward(&d, &t[0], &t[1], &t[2], output, logsumexp, mask, stream);
+}
+
 // =========================================================================================
 // Host utilities.
 extern "C" int mfa_masking_sequence_bucket(int sequence_length) {

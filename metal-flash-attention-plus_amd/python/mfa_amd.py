@@ -406,6 +406,9 @@ _sig("mfa_quantized_plan", ctypes.c_int,
 _sig("mfa_quantized_forward", ctypes.c_int,
      [_P(QuantizedDescriptor), _P(QuantizedTensor), _P(QuantizedTensor), _P(QuantizedTensor),
       _V, _V, _V, _V])
+_sig("mfa_quantized_forward_from_float", ctypes.c_int,
+     [_P(QuantizedDescriptor), _V, _V, _V, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+      ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _V, _V, _V, _V])
 _sig("mfa_quantized_backward_query", ctypes.c_int,
      [_P(QuantizedDescriptor), _P(QuantizedTensor), _P(QuantizedTensor), _P(QuantizedTensor),
       _V, _V, _V, _V, _V, _V])
@@ -604,6 +607,22 @@ class QuantizedAttention:
         check(lib.mfa_quantized_forward(ctypes.byref(desc), ctypes.byref(query),
                                         ctypes.byref(key), ctypes.byref(value), _ptr(output),
                                         _ptr(logsumexp), _ptr(mask), _stream(stream)))
+
+    def forward_from_buffers(self, desc: QuantizedDescriptor, query, key, value, output,
+                             target: Precision, mode: "QuantMode" = None, block_size=0,
+                             logsumexp=None, mask=None, stream=None, precisions=None):
+        """forward(queryBuffer:keyBuffer:valueBuffer:...:targetQuantization:quantizationMode:
+        descriptor:) (QuantizedAttention.swift:278-372): FP32/FP16/BF16 device tensors,
+        quantized on the GPU to `target`, then the quantized forward."""
+        import torch
+        tp = {torch.float32: Precision.FP32, torch.float16: Precision.FP16,
+              torch.bfloat16: Precision.BF16}
+        qp, kp, vp = precisions or (tp[query.dtype], tp[key.dtype], tp[value.dtype])
+        mode = QuantMode.tensorWise if mode is None else mode
+        check(lib.mfa_quantized_forward_from_float(
+            ctypes.byref(desc), _ptr(query), _ptr(key), _ptr(value), int(qp), int(kp), int(vp),
+            int(target), int(mode), int(block_size), _ptr(output), _ptr(logsumexp), _ptr(mask),
+            _stream(stream)))
 
     def backwardQuery(self, desc, query, key, value, output, grad_output, logsumexp, grad_query,
                       d_values, stream=None):

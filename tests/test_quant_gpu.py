@@ -718,3 +718,60 @@ def test_transposed_quantized_kv_matches_row_major(gpu, blockwise, kv):
     for o in outs:
         assert torch.isfinite(o).all()
         assert maxerr(o, ref) < 5e-3
+
+
+@pytest.mark.parametrize("target,mode,bs", [(P.INT8, mfa.QuantMode.tensorWise, 0),
+                                            (P.INT4, mfa.QuantMode.tensorWise, 0),
+                                            (P.INT8, mfa.QuantMode.blockwise, 32)])
+@pytest.mark.parametrize("src", [torch.float16, torch.float32])
+def test_forward_from_float_buffers(gpu, target, mode, bs, src):
+    # QuantizedAttention.forward(queryBuffer:...:targetQuantization:quantizationMode:descriptor:)
+    # (QuantizedAttention.swift:278-336): the C-ABI entry quantizes Q, K, V on the GPU and runs
+    # the quantized forward; it must equal mfa_quantize of each tensor followed by
+    # mfa_quantized_forward on the results, bit for bit.
+    B, H, Hkv, S, D = 1, 4, 2, 256, 64
+    g = torch.Generator(device=DEV).manual_seed(3)
+    q = torch.randn((B, H, S, D), generator=g, device=DEV).to(src)
+    k = torch.randn((B, Hkv, S, D), generator=g, device=DEV).to(src)
+    v = torch.randn((B, Hkv, S, D), generator=g, device=DEV).to(src)
+    base = mfa.AttentionDescriptor.make(S, S, D, causal=True)
+    desc = mfa.quantized_descriptor(base, target, target, target, B=B, H=H, Hkv=Hkv)
+    o1 = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
+    qa = mfa.QuantizedAttention()
+    qa.forward_from_buffers(desc, q, k, v, o1, target, mode, bs)
+    torch.cuda.synchronize()
+    keep = []
+
+    def manual(x):
+        rows = x.numel() // D
+        data, sc, bsc, bzp = mfa.quantize(x.reshape(-1), target, mode, rows, D, bs)
+        torch.cuda.synchronize()
+        keep.append((data, sc, bsc, bzp))
+        if mode == mfa.QuantMode.blockwise:
+            return mfa.quantized_tensor(data, target, block_scales=bsc, block_zero_points=bzp,
+                                        block_size=bs)
+        return mfa.quantized_tensor(data, target, scale=sc.item())
+
+    o2 = torch.full_like(o1, float("nan"))
+    qa.forward(desc, manual(q), manual(k), manual(v), o2)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o1).all()
+    assert torch.equal(o1, o2)
+    # And the reference's gate against the unquantized inputs (QuantizedAttentionTest.swift:519).
+    ref = ol.attention(q.float().cpu().numpy(), k.float().cpu().numpy(), v.float().cpu().numpy(),
+                       causal=True)["O"]
+    assert relerr(o1, ref) < (0.25 if target == P.INT8 else 0.6)
+
+
+def test_forward_from_float_buffers_wraps_unquantized_target(gpu):
+    # A target without quantization parameters wraps the buffers (:425-441): the FP16 forward.
+    B, H, S, D = 1, 2, 128, 64
+    g = torch.Generator(device=DEV).manual_seed(4)
+    q, k, v = (torch.randn((B, H, S, D), generator=g, device=DEV).half() for _ in range(3))
+    base = mfa.AttentionDescriptor.make(S, S, D)
+    desc = mfa.quantized_descriptor(base, P.INT8, P.INT8, P.INT8, B=B, H=H)
+    o1 = torch.empty((B, H, S, D), dtype=torch.float32, device=DEV)
+    mfa.QuantizedAttention().forward_from_buffers(desc, q, k, v, o1, P.FP16)
+    torch.cuda.synchronize()
+    ref = ol.attention(*(t.float().cpu().numpy() for t in (q, k, v)))["O"]
+    assert maxerr(o1, ref) < 5e-3
