@@ -824,6 +824,12 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
   const char* var = getenv("MFA_FWD_VARIANT");
+  if (const char* aw = getenv("MFA_FWD_AW")) {
+    if (aw[0] == '1') {
+      const hipError_t e = fwd_aw_dispatch(p, elem, DP, stream);
+      if (e != hipErrorNotSupported) return e;
+    }
+  }
   const int blocks = p.nblk * p.B * p.H;
   // Causal: mirrored pairs while they fill at most ~1.5 rounds of the chip, or up to 3 rounds
   // for long rows (S >= 8192: 64 blocks; one-process A/B: H16 S8192 1057 vs 987 TF single,

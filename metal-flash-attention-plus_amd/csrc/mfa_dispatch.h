@@ -77,6 +77,9 @@ size_t fwd_stream_workspace_bytes(const FwdParams& p, int elem, int DP, size_t* 
 hipError_t fwd_stream_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
+// One wave per SIMD, two query sub-blocks per wave, O in kernel-owned AGPRs
+// (attention_fwd_aw.hip): D = 128, no mask or causal.
+hipError_t fwd_aw_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Dense 16-bit copy [B, Hx, S, D] of a quantised operand holding the MFMA operands the
 // dequantise-on-load staging would produce (kv_dequant.hip).
 hipError_t kv_dequant_dispatch(const Operand& op, int B, int Hx, int S, int D, int elem,
