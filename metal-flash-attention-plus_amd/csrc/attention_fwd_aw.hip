@@ -61,9 +61,6 @@
 #endif
 
 namespace mfa {
-#ifdef AW_DEBUG_TRACE
-__device__ float g_aw_trace[256];
-#endif
 namespace aw {
 
 // Every O register, named as a clobber of each inline-assembly statement that writes O: the
@@ -108,26 +105,22 @@ __device__ __forceinline__ void settle_writes() { asm volatile("s_nop 4" ::: "me
 
 // O^T tile (rows of the head dimension, query on the lane) += V^T · P^T into a[R:R+15].
 // NOP: the chain's first MFMA, whose P operand the VALU may have written just before.
-// `keep`: the previous MFMA's P operand, held live until this MFMA issues.  The compiler sees
-// an inline-assembly MFMA as done with its inputs when it issues, and may let the next VALU
-// write their registers; the matrix core reads its B operand after issue, so a P register
-// rewritten right behind its MFMA (the next tile's P packed in place) would be read late.
 template <class E, int R, bool NOP>
-__device__ __forceinline__ void pv_mfma(i16x8 a, i16x8 b, i16x8 keep, i16x8 keepa) {
+__device__ __forceinline__ void pv_mfma(i16x8 a, i16x8 b) {
   if constexpr (E::prec == P_FP16) {
     if constexpr (NOP)
       asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 a[%2:%2+15], %0, %1, a[%2:%2+15]" ::"v"(a),
-                   "v"(b), "n"(R), "v"(keep), "v"(keepa) : AW_O_CLOBBERS);
+                   "v"(b), "n"(R) : AW_O_CLOBBERS);
     else
       asm volatile("v_mfma_f32_32x32x16_f16 a[%2:%2+15], %0, %1, a[%2:%2+15]" ::"v"(a), "v"(b),
-                   "n"(R), "v"(keep), "v"(keepa) : AW_O_CLOBBERS);
+                   "n"(R) : AW_O_CLOBBERS);
   } else {
     if constexpr (NOP)
       asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%2:%2+15], %0, %1, a[%2:%2+15]" ::"v"(a),
-                   "v"(b), "n"(R), "v"(keep), "v"(keepa) : AW_O_CLOBBERS);
+                   "v"(b), "n"(R) : AW_O_CLOBBERS);
     else
       asm volatile("v_mfma_f32_32x32x16_bf16 a[%2:%2+15], %0, %1, a[%2:%2+15]" ::"v"(a), "v"(b),
-                   "n"(R), "v"(keep), "v"(keepa) : AW_O_CLOBBERS);
+                   "n"(R) : AW_O_CLOBBERS);
   }
 }
 
@@ -163,7 +156,6 @@ struct Soft {
   float rs[4];
   float pe;            // the even value of the pair being packed
   u32x4 pw[BK / 16];   // packed P, two 16-bit values per word (Arith16::pack order)
-  unsigned pt[2];      // words of the next tile's P held until the PV chain frees pw[0]
   __device__ __forceinline__ i16x8 pb(int ks) const { return __builtin_bit_cast(i16x8, pw[ks]); }
   __device__ __forceinline__ void reset() { rs[0] = rs[1] = rs[2] = rs[3] = 0.f; }
 };
@@ -212,20 +204,16 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
   using A = Arith16<E, DP>;
   using aw::aread;
   using aw::sfor;
-  using T_ = std::true_type;
-  using F_ = std::false_type;
   constexpr bool PS = E::prec == P_FP16 && DP <= 128;
   constexpr int NJ = BK / 32, ND = DP / 32, DS = DP / 16;
   constexpr int NV = NJ * 16;                  // S values of a tile per lane (half its keys)
-  constexpr int HV = NV / 2;                   // values of a sub-block per phase
+  constexpr int HV = NV / 2;                   // values per half pass (one per MFMA of a chain)
   constexpr int TILEB = BK * DP * 2;
   constexpr int SLOT = (MIRROR ? 2 : 1) * TILEB;  // phase 2 stages two tiles per step
   constexpr float THR = 8.0f;
-  constexpr int NKF = DS * NJ, NVF = NJ * 2 * ND;  // K / V fragments of a tile
-  constexpr int NM = 2 * NKF;                  // MFMAs per phase (both sub-blocks)
-  static_assert(DP == 128 && NKF == 16 && NVF == 16 && NM == 2 * HV, "one softmax value per MFMA gap");
+  constexpr int NQK = DS * NJ, NPV = NJ * 2 * ND;
+  static_assert(DP == 128 && HV == NQK && HV == NPV, "one value per MFMA of each chain");
   constexpr int OB0 = 0, OB1 = 64;             // AGPR bases of X0's and X1's O
-  constexpr int AHK = AW_AHK, AHV = AW_AHV;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const kring = smem;                    // K slots 0, 1
   char* const vring = smem + 2 * SLOT;         // V slots 0, 1, 2
@@ -269,24 +257,17 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
   const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
   const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
 
-  // First key of X1's / X0's tile at step u (the same tile in phase 1).
+  // First key of X1's / X0's tile at step u.
   auto key1 = [&](int u) __attribute__((always_inline)) { return kb0 + (u < nA ? u : nA + 2 * (u - nA)) * BK; };
   auto key0 = [&](int u) __attribute__((always_inline)) { return kb0 + (u < nA ? u : nA + 2 * (u - nA) + 1) * BK; };
-  auto kslot = [&](int u) __attribute__((always_inline)) { return kring + (u & 1) * SLOT; };
-  auto vslot = [&](int u) __attribute__((always_inline)) { return vring + (u % 3) * SLOT; };
-  auto dma_k = [&](int u) __attribute__((always_inline)) {
-    kd.issue(khead, key1(u), kslot(u));
-    if (MIRROR && u >= nA) kd.issue(khead, key0(u), kslot(u) + TILEB);
-  };
-  auto dma_v = [&](int u) __attribute__((always_inline)) {
-    vd.issue(vhead, key1(u), vslot(u));
-    if (MIRROR && u >= nA) vd.issue(vhead, key0(u), vslot(u) + TILEB);
-  };
 
-  // Prologue: K of steps 0 and 1 and V of step 0, then both sub-blocks' Q rows.
-  dma_k(0);
-  dma_v(0);
-  if (U > 1) dma_k(1);
+  // Prologue: step 0's tiles, then both sub-blocks' Q rows into registers.
+  kd.issue(khead, key1(0), kring);
+  vd.issue(vhead, key1(0), vring);
+  if (nA == 0) {
+    kd.issue(khead, key0(0), kring + TILEB);
+    vd.issue(vhead, key0(0), vring + TILEB);
+  }
   i16x8 qf0[DS], qf1[DS];
   load_q2_raw<DP>(qf0, p, b, h, q00 + l32, q00 + l32 < p.R, hh);
   load_q2_raw<DP>(qf1, p, b, h, qB0 + l32, qB0 + l32 < p.R, hh);
@@ -295,11 +276,7 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
   st1.init();
   aw::zero_o<0, 128>();
   aw::Soft<BK> sm0, sm1;
-  sm0.reset();
-  sm1.reset();
-  // S of the current step (written by phase A) and the half of the previous step's S whose
-  // values phase A's gaps still carry (key block 1).
-  f32x16 sc0[NJ], sc1[NJ], sp0[NJ], sp1[NJ];
+  f32x16 s0[NJ], s1[NJ];
   wait_vm();
   prescale_q2<E, DP>(qf0, c);
   prescale_q2<E, DP>(qf1, c);
@@ -307,92 +284,63 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
   __syncthreads();
   AW_ACC_DECL();
 
-  // Fragment streams.  Phase A (S = K·Q^T for both sub-blocks) reads each K fragment once for
-  // both when they share a tile (SH), in key-block-major order (all of S[0] first); phase B
-  // (O^T += V^T·P^T for both) reads each V fragment once likewise.  A phase's last read-ahead
-  // slots prefetch the first fragments of the next phase (tail).
-  i16x8 kp[2 * AHK], vp[2 * AHV];
-  auto kread = [&](const char* kt, int f) __attribute__((always_inline)) {
-    return A::read_row_a(kt, rbase, f / DS, f % DS);
+  // Fragment rings of the two chain kinds.  A chain's last read-ahead slots prefetch the first
+  // fragments of the chain after it (tail(j), j < AH), so no chain but the iteration's first
+  // (whose K tile is only valid after the barrier) starts on an LDS read's latency.
+  constexpr int AHK = AW_AHK, AHV = AW_AHV;
+  i16x8 kp[AHK], vp[AHV];
+  auto kread = [&](const char* kt, int i) __attribute__((always_inline)) {
+    return A::read_row_a(kt, rbase, i % NJ, i / NJ);
   };
-  auto vread = [&](const char* vt, int f) __attribute__((always_inline)) {
-    const int jk = f / ND, dt = f % ND;
+  auto vread = [&](const char* vt, int i) __attribute__((always_inline)) {
+    const int jk = i / ND, dt = i % ND;
     return A::read_tr_a(vt, trb, (jk >> 1) * 32, jk & 1, dt * 32);
   };
-  // Load n of a phase's stream: fragment n / 2 of sub-block n % 2's tile (not shared), or
-  // fragment n (shared).
-  auto kload = [&](auto sh_c, const char* k0t, const char* k1t, int n) __attribute__((always_inline)) {
-    if constexpr (decltype(sh_c)::value) kp[n % AHK] = kread(k1t, n);
-    else kp[n % (2 * AHK)] = kread((n & 1) ? k1t : k0t, n >> 1);
-  };
-  auto vload = [&](auto sh_c, const char* v0t, const char* v1t, int n) __attribute__((always_inline)) {
-    if constexpr (decltype(sh_c)::value) vp[n % AHV] = vread(v1t, n);
-    else vp[n % (2 * AHV)] = vread((n & 1) ? v1t : v0t, n >> 1);
-  };
   auto no_tail = [](int) __attribute__((always_inline)) {};
-
-  // Phase A: MFMA i updates S[j] of sub-block x = i % 2 with fragment f = i / 2 (j = f / DS).
-  auto phase_a = [&](auto sh_c, const char* k0t, const char* k1t, auto&& hook, auto&& tail)
-                     __attribute__((always_inline)) {
-    constexpr bool SH = decltype(sh_c)::value;
-    constexpr int NL = SH ? NKF : 2 * NKF, AH = SH ? AHK : 2 * AHK;
+  // S^T = K·Q^T (key in registers, query on the lane; Q pre-scaled by c on the fp16 path).
+  // PRE: kp already holds the chain's first AHK fragments.
+  auto qk = [&](auto pre_c, const char* kt, const i16x8 (&qf)[DS], const aw::Row& st,
+                f32x16 (&s)[NJ], auto&& hook, auto&& tail) __attribute__((always_inline)) {
+    if constexpr (!decltype(pre_c)::value) {
 #pragma unroll
-    for (int i = 0; i < NM; ++i) {
-      const int f = i / 2, x = i % 2, j = f / DS, ds = f % DS;
-      const i16x8 kf = SH ? kp[f % AHK] : kp[i % (2 * AHK)];
-      f32x16 (&s)[NJ] = x ? sc1 : sc0;
-      s[j] = A::mma(kf, x ? qf1[ds] : qf0[ds], ds == 0 ? zero16() : s[j]);
-      const int n = SH ? f : i;  // the load this MFMA consumed last
-      if (!SH || x == 1) {
-        if (n + AH < NL) kload(sh_c, k0t, k1t, n + AH);
-        else tail(n + AH - NL);
-      }
+      for (int i = 0; i < AHK; ++i) kp[i] = kread(kt, i);
+    }
+#pragma unroll
+    for (int i = 0; i < NQK; ++i) {
+      const int ds = i / NJ, j = i % NJ;
+      if (ds == 0)
+        s[j] = A::mma(kp[i % AHK], qf[0], zero16());
+      else
+        s[j] = A::mma(kp[i % AHK], qf[ds], s[j]);
+      if (i + AHK < NQK) kp[i % AHK] = kread(kt, i + AHK);
+      else tail(i + AHK - NQK);
       hook(i);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // Phase B: MFMA i adds V fragment f = i / 2 times P of sub-block x = i % 2 to its O.
-  auto phase_b = [&](auto sh_c, const char* v0t, const char* v1t, auto&& hook, auto&& tail)
-                     __attribute__((always_inline)) {
-    constexpr bool SH = decltype(sh_c)::value;
-    constexpr int NL = SH ? NVF : 2 * NVF, AH = SH ? AHV : 2 * AHV;
-    i16x8 vprev = SH ? vp[0] : vp[0];
-    sfor<0, NM>([&](auto ic) {
-      constexpr int i = decltype(ic)::value, f = i / 2, x = i % 2, jk = f / ND, dt = f % ND;
-      const i16x8 vf = SH ? vp[f % AHV] : vp[i % (2 * AHV)];
-      constexpr int ip = i > 0 ? i - 1 : 0, jkp = (ip / 2) / ND;
-      aw::pv_mfma<E, (x ? OB1 : OB0) + 16 * dt, i == 0>(vf, x ? sm1.pb(jk) : sm0.pb(jk),
-                                                      (ip & 1) ? sm1.pb(jkp) : sm0.pb(jkp), vprev);
-      vprev = vf;
-      if constexpr (i == NM - 1) asm volatile("s_nop 3" ::"v"(vf), "v"(x ? sm1.pb(jk) : sm0.pb(jk)));
-      constexpr int n = SH ? f : i;
-      if constexpr (!SH || x == 1) {
-        if constexpr (n + AH < NL) vload(sh_c, v0t, v1t, n + AH);
-        else tail(n + AH - NL);
-      }
+  // O^T += V^T·P^T into the sub-block's AGPRs.  PRE: vp holds the first AHV fragments.
+  auto pv = [&](auto ob_c, auto pre_c, const char* vt, const aw::Soft<BK>& sm, auto&& hook,
+                auto&& tail) __attribute__((always_inline)) {
+    constexpr int OB = decltype(ob_c)::value;
+    if constexpr (!decltype(pre_c)::value) {
+#pragma unroll
+      for (int i = 0; i < AHV; ++i) vp[i] = vread(vt, i);
+    }
+    sfor<0, NPV>([&](auto ic) {
+      constexpr int i = decltype(ic)::value, jk = i / ND, dt = i % ND;
+      aw::pv_mfma<E, OB + 16 * dt, i == 0>(vp[i % AHV], sm.pb(jk));
+      if constexpr (i + AHV < NPV) vp[i % AHV] = vread(vt, i + AHV);
+      else tail(i + AHV - NPV);
       hook(i);
       __builtin_amdgcn_sched_barrier(0);
     });
-  };
-  auto kpre = [&](auto sh_c, const char* k0t, const char* k1t) __attribute__((always_inline)) {
-    constexpr int AH = decltype(sh_c)::value ? AHK : 2 * AHK;
-    return [&, sh_c, k0t, k1t](int j) __attribute__((always_inline)) {
-      if (j < AH) kload(sh_c, k0t, k1t, j);
-    };
-  };
-  auto vpre = [&](auto sh_c, const char* v0t, const char* v1t) __attribute__((always_inline)) {
-    constexpr int AH = decltype(sh_c)::value ? AHV : 2 * AHV;
-    return [&, sh_c, v0t, v1t](int j) __attribute__((always_inline)) {
-      if (j < AH) vload(sh_c, v0t, v1t, j);
-    };
   };
 
   // Value k of a sub-block's tile: P = exp2(S·c − m) against the row max the decision before
   // the pass settled, row-sum partial, packed in place by pairs (the order of Arith16::pack).
   // The empty volatile statements pin each value where it is computed, in the MFMA gap it was
-  // placed in; without them the compiler moves the sums and packs into bursts between phases.
-  auto smv = [&](f32x16 (&s)[NJ], aw::Soft<BK>& sm, const aw::Row& st, int k, bool hold = false)
-                 __attribute__((always_inline)) {
+  // placed in; without them the compiler moves the sums and packs into bursts between chains.
+  auto smv = [&](f32x16 (&s)[NJ], aw::Soft<BK>& sm, const aw::Row& st, int k) __attribute__((always_inline)) {
     const int j = k >> 4, i = k & 15;
     const float v = s[j][i];
     float pv = __builtin_amdgcn_exp2f(PS ? v - st.m : __builtin_fmaf(v, c, -st.m));
@@ -404,60 +352,38 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
     } else {
       unsigned pk = aw::pack2<E>(sm.pe, pv);
       asm volatile("" : "+v"(pk));
-      if (hold) sm.pt[(k & 7) >> 1] = pk;
-      else sm.pw[k >> 3][(k & 7) >> 1] = pk;
+      sm.pw[k >> 3][(k & 7) >> 1] = pk;
     }
-  };
-  // Gap i of phase B carries value i / 2 of the current S of sub-block i % 2; gap i of phase A
-  // value HV + i / 2 of the previous S.
-  // Phase B's MFMAs 0..7 still read the previous tile's P word block 0: the words its gaps
-  // 0..7 complete are held and written at gap 8.
-  auto gap_cur = [&](int i) __attribute__((always_inline)) {
-    if (i & 1) smv(sc1, sm1, st1, i / 2, i < 8);
-    else smv(sc0, sm0, st0, i / 2, i < 8);
-    if (i == 8) {
-      sm0.pw[0][0] = sm0.pt[0];
-      sm0.pw[0][1] = sm0.pt[1];
-      sm1.pw[0][0] = sm1.pt[0];
-      sm1.pw[0][1] = sm1.pt[1];
-    }
-  };
-  auto gap_prev = [&](int i) __attribute__((always_inline)) {
-    if (i & 1) smv(sp1, sm1, st1, HV + i / 2);
-    else smv(sp0, sm0, st0, HV + i / 2);
   };
   // The tile's row max (both lane halves), then the lazy-rescale decision (wave-uniform,
-  // rarely taken).  Only the row state changes here; O is scaled after the phase that adds the
-  // previous tile's P (corr, returned; 1 = nothing to do).
-  auto decide = [&](const f32x16 (&s)[NJ], aw::Row& st) __attribute__((always_inline)) {
+  // rarely taken): only the row state and the sub-block's O in AGPRs change in the branch.
+  auto decide = [&](auto ob_c, const f32x16 (&s)[NJ], aw::Row& st) __attribute__((always_inline)) {
+    constexpr int OB = decltype(ob_c)::value;
     float a4[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int jj = q >> 1, i0 = (q & 1) * 8;
-      float m0 = __builtin_fmaxf(__builtin_fmaxf(s[jj][i0], s[jj][i0 + 1]), s[jj][i0 + 2]);
-      m0 = __builtin_fmaxf(__builtin_fmaxf(m0, s[jj][i0 + 3]), s[jj][i0 + 4]);
-      m0 = __builtin_fmaxf(__builtin_fmaxf(m0, s[jj][i0 + 5]), s[jj][i0 + 6]);
-      a4[q] = __builtin_fmaxf(m0, s[jj][i0 + 7]);
+      const int k0 = 8 * q;
+      float m0 = __builtin_fmaxf(__builtin_fmaxf(s[k0 >> 4][(k0 & 15)], s[k0 >> 4][(k0 & 15) + 1]),
+                                 s[k0 >> 4][(k0 & 15) + 2]);
+      m0 = __builtin_fmaxf(__builtin_fmaxf(m0, s[k0 >> 4][(k0 & 15) + 3]), s[k0 >> 4][(k0 & 15) + 4]);
+      m0 = __builtin_fmaxf(__builtin_fmaxf(m0, s[k0 >> 4][(k0 & 15) + 5]), s[k0 >> 4][(k0 & 15) + 6]);
+      a4[q] = __builtin_fmaxf(m0, s[k0 >> 4][(k0 & 15) + 7]);
     }
     const float mx = cross_half_max(__builtin_fmaxf(__builtin_fmaxf(a4[0], a4[1]), __builtin_fmaxf(a4[2], a4[3])));
     const float mt = PS ? mx : mx * c;
-    bool scale = false;
-    float corr = 1.f;
     if (__builtin_expect(__any(mt > st.m + THR), 0)) {
       MFA_KEEP_BRANCH();
       const float m_new = fmaxf(st.m, mt);
-      corr = __builtin_amdgcn_exp2f(st.m - m_new);
+      const float corr = __builtin_amdgcn_exp2f(st.m - m_new);
       // Rows still at the initial max have O = 0 (every P so far was exp2(-inf)): no multiply.
-      scale = !__all(st.m == -kFltMax);
+      if (!__all(st.m == -kFltMax)) aw::scale_o<OB>(corr);
       st.m = m_new;
       st.lh *= corr;
     }
-    return scale ? corr : 1.f;
   };
   // After the tile's last value: l += Σ P.
   auto finish = [&](aw::Soft<BK>& sm, aw::Row& st) __attribute__((always_inline)) {
     st.lh += (sm.rs[0] + sm.rs[1]) + (sm.rs[2] + sm.rs[3]);
-    sm.reset();
   };
   // Causal diagonal / key-edge masks of a sub-block's tile (keys t..t+BK-1, rows q0 + l32).
   auto mask = [&](f32x16 (&s)[NJ], int t, int q0) __attribute__((always_inline)) {
@@ -470,8 +396,8 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
     }
   };
   // O of X0 (a[0:63]) straight to global memory, row per lane (the phase switch).
-  auto store_x0 = [&](float m, float lh, int q0) __attribute__((always_inline)) {
-    float l = cross_half_sum(lh) + kFltMin;
+  auto store_x0 = [&](const aw::Row& st, int q0) __attribute__((always_inline)) {
+    float l = cross_half_sum(st.lh) + kFltMin;
     if (!(l > 0.f)) l = kFltMin;
     const float inv = p.o_mul / l;
     const int qi = q0 + l32;
@@ -485,163 +411,143 @@ __global__ void __launch_bounds__(256, 1) mfa_fwd_aw_kernel(FwdParams p) {
         const float x0 = aread<r>(), x1 = aread<r + 1>(), x2 = aread<r + 2>(), x3 = aread<r + 3>();
         if (d < p.D) st_o4<false>(orow + d, x0 * inv, x1 * inv, x2 * inv, x3 * inv);
       });
-      if (hh == 0) store_l(p, m + __log2f(l), b, h, qi);
-    }
-  };
-  // DMA pieces of a phase B: K of step u + 2 and V of step u + 1, one piece every other gap.
-  auto dma_gap = [&](int u, int i) __attribute__((always_inline)) {
-    if ((i & 1) == 0) {
-      const int pc = i >> 1, which = pc & 3, k = pc >> 2;  // 16 slots: K1 V1 K0 V0 x 4
-      const int uk = u + 2, uv = u + 1;
-      if (which == 0 && uk < U) kd.issue_piece(khead, key1(uk), kslot(uk), k);
-      if (which == 1 && uv < U) vd.issue_piece(vhead, key1(uv), vslot(uv), k);
-      if (which == 2 && MIRROR && uk < U && uk >= nA) kd.issue_piece(khead, key0(uk), kslot(uk) + TILEB, k);
-      if (which == 3 && MIRROR && uv < U && uv >= nA) vd.issue_piece(vhead, key0(uv), vslot(uv) + TILEB, k);
+      if (hh == 0) store_l(p, st.m + __log2f(l), b, h, qi);
     }
   };
 
-  float mA = 0.f, lA = 0.f;  // A's row state at the phase switch
-  // Step u: phase A(u) [values HV.. of S(u-1)]; decisions on S(u); barrier; phase B(u): PV(u-1)
-  // [values 0..HV-1 of S(u); DMA]; O scaled for decisions of u.
-  auto step = [&](int u, auto first_c, auto sh_c, auto shp_c) __attribute__((always_inline)) {
+  int vcur = 0;  // V slot of step u (u % 3)
+  auto iteration = [&](int u, auto first_c, auto dma2_c) __attribute__((always_inline)) {
     constexpr bool FIRST = decltype(first_c)::value;
-    constexpr bool SH = decltype(sh_c)::value;    // X0 and X1 read one K tile at step u
-    constexpr bool SHP = decltype(shp_c)::value;  // ... and one V tile at step u - 1
-    const bool sw = MIRROR && u == nA && nA > 0;
-    if (sw) {
-#pragma unroll
-      for (int ds = 0; ds < DS; ++ds) qf0[ds] = qf1[ds];
-    }
-    const char* kt1 = kslot(u);
-    const char* kt0 = kt1 + (SH ? 0 : TILEB);
-    const char* vt1 = vslot(u - 1);
-    const char* vt0 = vt1 + (SHP ? 0 : TILEB);
-    if constexpr (FIRST) {
-#pragma unroll
-      for (int j = 0; j < (SH ? AHK : 2 * AHK); ++j) kload(sh_c, kt0, kt1, j);
-      phase_a(sh_c, kt0, kt1, no_tail, no_tail);
-    } else {
-#ifdef AW_DBG_NOPRE
-      if constexpr (!SH) {
-#pragma unroll
-        for (int j = 0; j < 2 * AHK; ++j) kload(sh_c, kt0, kt1, j);
-      }
-#endif
-      phase_a(sh_c, kt0, kt1, gap_prev, vpre(shp_c, vt0, vt1));
-    }
-    AW_ACC(0);
-    if constexpr (!FIRST) {
-      finish(sm0, st0);
-      finish(sm1, st1);
-    }
-    if (sw) {  // A's last values are summed: keep its state, X0 starts B's second state
-      mA = st0.m;
-      lA = st0.lh;
+    constexpr bool DMA2 = decltype(dma2_c)::value;  // step u + 1 stages two tiles
+    const bool ph2 = u >= nA;
+    if (MIRROR && u == nA && nA > 0) {
+      // A is complete (its last PV ran in iteration u - 1): store it, then X0 becomes a second
+      // state of B's rows.
+      store_x0(st0, q00);
       st0.init();
-      q00 = qB0;
-    }
-    mask(sc0, key0(u), q00);
-    mask(sc1, key1(u), qB0);
-    const float corr0 = decide(sc0, st0);
-    const float corr1 = decide(sc1, st1);
-#ifdef AW_DEBUG_TRACE
-    if (blockIdx.x == 0 && tid == 0 && u < 16) {
-      g_aw_trace[u * 8 + 0] = st0.m; g_aw_trace[u * 8 + 1] = st0.lh; g_aw_trace[u * 8 + 2] = corr0;
-      g_aw_trace[u * 8 + 3] = st1.m; g_aw_trace[u * 8 + 4] = st1.lh; g_aw_trace[u * 8 + 5] = corr1;
-    }
-#endif
-    AW_ACC(1);
-    wait_vm();
-    AW_ACC(2);
-    __syncthreads();
-    AW_ACC(3);
-    // K of step u + 1 is now valid for every wave: phase B's tail may prefetch it.
-    const bool shn = !MIRROR || u + 1 < nA;
-    const char* kn1 = kslot(u + 1);
-    const char* kn0 = kn1 + (shn ? 0 : TILEB);
-    auto tail = [&](int j) __attribute__((always_inline)) {
-#ifdef AW_DBG_NOPRE
-      if (!shn) return;
-#endif
-      if (u + 1 < U) {
-        if (shn) kpre(T_(), kn0, kn1)(j);
-        else kpre(F_(), kn0, kn1)(j);
-      }
-    };
-    if constexpr (FIRST) {
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        gap_cur(i);
-        dma_gap(u, i);
-      }
-#pragma unroll
-      for (int j = 0; j < 2 * AHK; ++j) tail(j);
-    } else {
-      phase_b(shp_c, vt0, vt1, [&](int i) __attribute__((always_inline)) {
-        gap_cur(i);
-        dma_gap(u, i);
-      }, [&](int j) __attribute__((always_inline)) {
-        // Phase B's tail has fewer slots than phase A needs: its last one loads the rest.
-        constexpr int AHB = SHP ? AHV : 2 * AHV;
-        if (j < AHB - 1) tail(j);
-        else if (j == AHB - 1) {
-#pragma unroll
-          for (int r = AHB - 1; r < 2 * AHK; ++r) tail(r);
-        }
-      });
-    }
-    AW_ACC(4);
-    if (sw) {  // A's last P has been added (PV(u - 1) above): A leaves, X0's O restarts
-      store_x0(mA, lA, rbA * 128 + 32 * w);
       aw::zero_o<OB0, 64>();
       aw::settle_writes();
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) qf0[ds] = qf1[ds];
+      q00 = qB0;
     }
-    if (__builtin_expect(corr0 != 1.f, 0)) aw::scale_o<OB0>(corr0);
-    if (__builtin_expect(corr1 != 1.f, 0)) aw::scale_o<OB1>(corr1);
-#ifdef AW_DEBUG_TRACE
-    {
-      aw::drain_mfma();
-      const float a0v = aread<0>(), a64v = aread<64>();
-      if (blockIdx.x == 0 && tid == 0 && u < 16) { g_aw_trace[u * 8 + 6] = a0v; g_aw_trace[u * 8 + 7] = a64v; }
+    const char* kt1 = kring + (u & 1) * SLOT;
+    const char* kt0 = kt1 + (ph2 ? TILEB : 0);
+    const int vprev = vcur == 0 ? 2 : vcur - 1;
+    const char* vt1 = vring + vprev * SLOT;                     // X1's tile of step u - 1
+    const char* vt0 = vring + vcur * SLOT + (ph2 ? TILEB : 0);  // X0's tile of step u
+    const int vnext = vcur == 2 ? 0 : vcur + 1;
+    char* const kn = kring + ((u + 1) & 1) * SLOT;
+    char* const vn = vring + vnext * SLOT;
+    const int tn1 = key1(u + 1), tn0 = key0(u + 1);
+    // The next step's tiles: 4 pieces per wave per tile, one every few MFMA gaps.
+    constexpr int NP = DMA2 ? 16 : 8;
+    constexpr int NCH = DMA2 ? 4 : AW_DMA_CHAINS;  // chains that carry the pieces
+    constexpr int STRIDE = NCH * NQK / NP;         // gaps per piece
+    auto dma = [&](int chain, int i) __attribute__((always_inline)) {
+      const int g = chain * NQK + i;
+      if (g < NCH * NQK && g % STRIDE == STRIDE / 2) {
+        const int pc = g / STRIDE, which = pc / 4, k = pc % 4;
+        if (which == 0) kd.issue_piece(khead, tn1, kn, k);
+        else if (which == 1) vd.issue_piece(vhead, tn1, vn, k);
+        else if (which == 2) kd.issue_piece(khead, tn0, kn + TILEB, k);
+        else vd.issue_piece(vhead, tn0, vn + TILEB, k);
+      }
+    };
+    const int t0 = key0(u), t1 = key1(u);
+    using O0 = std::integral_constant<int, OB0>;
+    using O1 = std::integral_constant<int, OB1>;
+
+    auto pre_v = [&](const char* vt) __attribute__((always_inline)) {
+      return [&, vt](int j) __attribute__((always_inline)) { if (j < AHV) vp[j] = vread(vt, j); };
+    };
+    auto pre_k = [&](const char* kt, bool from_pv) __attribute__((always_inline)) {
+      // A PV chain's tail has AHV < AHK slots: its last one loads the rest.
+      return [&, kt, from_pv](int j) __attribute__((always_inline)) {
+        kp[j] = kread(kt, j);
+        if (from_pv && j == AHV - 1) {
+#pragma unroll
+          for (int r = AHV; r < AHK; ++r) kp[r] = kread(kt, r);
+        }
+      };
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+
+    // QK_0(u) | second half of softmax_1(u - 1); its tail prefetches PV_1's (or, in the first
+    // iteration, QK_1's) first fragments.
+    auto h_qk0 = [&](int i) __attribute__((always_inline)) {
+      if constexpr (!FIRST) smv(s1, sm1, st1, HV + i);
+      dma(0, i);
+    };
+    if constexpr (FIRST) qk(F_(), kt0, qf0, st0, s0, h_qk0, pre_k(kt1, false));
+    else qk(F_(), kt0, qf0, st0, s0, h_qk0, pre_v(vt1));
+    AW_ACC(0);
+    if constexpr (!FIRST) finish(sm1, st1);
+    mask(s0, t0, q00);
+    decide(O0(), s0, st0);
+    sm0.reset();
+    AW_ACC(1);
+    if constexpr (!FIRST) {
+      // PV_1(u - 1) | first half of softmax_0(u).
+      pv(O1(), T_(), vt1, sm1, [&](int i) __attribute__((always_inline)) {
+        smv(s0, sm0, st0, i);
+        dma(1, i);
+      }, pre_k(kt1, true));
+      AW_ACC(2);
+    } else {
+#pragma unroll
+      for (int k = 0; k < HV; ++k) smv(s0, sm0, st0, k);
     }
-#endif
-    // The half of S whose values the next phase A carries.
-    sp0[NJ - 1] = sc0[NJ - 1];
-    sp1[NJ - 1] = sc1[NJ - 1];
+    // QK_1(u) | second half of softmax_0(u).
+    qk(T_(), kt1, qf1, st1, s1, [&](int i) __attribute__((always_inline)) {
+      smv(s0, sm0, st0, HV + i);
+      dma(2, i);
+    }, pre_v(vt0));
+    AW_ACC(3);
+    finish(sm0, st0);
+    mask(s1, t1, qB0);
+    decide(O1(), s1, st1);
+    sm1.reset();
+    AW_ACC(4);
+    // PV_0(u) | first half of softmax_1(u).
+    pv(O0(), T_(), vt0, sm0, [&](int i) __attribute__((always_inline)) {
+      smv(s1, sm1, st1, i);
+      dma(3, i);
+    }, no_tail);
     AW_ACC(5);
+    if constexpr (FIRST) {
+      // No PV_1(u - 1) chain carried its pieces.
+#pragma unroll
+      for (int i = 0; i < NQK; ++i) dma(1, i);
+    }
+    wait_vm();
+    AW_ACC(6);
+    __syncthreads();
+    AW_ACC(7);
+    vcur = vnext;
   };
 
+  using T_ = std::true_type;
+  using F_ = std::false_type;
   if (U > 0) {
-    if (nA == 0 && MIRROR) step(0, T_(), F_(), F_());
-    else step(0, T_(), T_(), T_());
+    // u + 1 stages two tiles once u + 1 >= nA (phase 2).
+    if (1 >= nA && MIRROR) iteration(0, T_(), T_());
+    else iteration(0, T_(), F_());
     int u = 1;
     if constexpr (MIRROR) {
-      for (; u < nA && u < U; ++u) step(u, F_(), T_(), T_());
-      if (u < U && u == nA && nA > 0) {
-        step(u, F_(), F_(), T_());  // the switch step: K tiles split, V still shared
-        ++u;
-      }
-      for (; u < U; ++u) step(u, F_(), F_(), F_());
+      for (; u < nA - 1 && u < U; ++u) iteration(u, F_(), F_());
+      for (; u < U; ++u) iteration(u, F_(), T_());
     } else {
-      for (; u < U; ++u) step(u, F_(), T_(), T_());
+      for (; u < U; ++u) iteration(u, F_(), F_());
     }
-    // Drain: values HV.. of S(U - 1), then PV(U - 1).
+    // Drain: the rest of softmax_1(U - 1) and PV_1(U - 1).
 #pragma unroll
-    for (int i = 0; i < NM; ++i) gap_prev(i);
-    finish(sm0, st0);
+    for (int k = HV; k < NV; ++k) smv(s1, sm1, st1, k);
     finish(sm1, st1);
-    const bool shl = !MIRROR || U - 1 < nA;
-    const char* vt1 = vslot(U - 1);
-    const char* vt0 = vt1 + (shl ? 0 : TILEB);
-    if (shl) {
-#pragma unroll
-      for (int j = 0; j < AHV; ++j) vload(T_(), vt0, vt1, j);
-      phase_b(T_(), vt0, vt1, no_tail, no_tail);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2 * AHV; ++j) vload(F_(), vt0, vt1, j);
-      phase_b(F_(), vt0, vt1, no_tail, no_tail);
-    }
+    const int vprev = vcur == 0 ? 2 : vcur - 1;
+    pv(std::integral_constant<int, OB1>(), std::false_type(), vring + vprev * SLOT, sm1, no_tail,
+       no_tail);
   }
 
   AW_ACC_END();

@@ -82,13 +82,13 @@ int main(int argc, char** argv) {
   CK(hipStreamSynchronize(st));
   CK(hipMemcpy(stamps.data(), dsym, sizeof(unsigned long long) << 20, hipMemcpyDeviceToHost));
   const int iters = causal ? 0 : S / 64;  // unmasked: one 64-key tile per iteration
-  const char* names[8] = {"phase A (QK)", "finish+mask+decide", "wait_vm", "barrier",
-                          "phase B (PV)", "scale+copy", "-", "-"};
+  const char* names[8] = {"QK_0 | sm_1", "mask+decide_1", "PV_1 | sm_0", "QK_1 | sm_0",
+                          "mask+decide_0", "PV_0 | sm_1", "wait_vm", "barrier"};
   double tot = 0;
   for (int s = 0; s < 8; ++s) {
     std::vector<double> x;
     for (int w = 0; w < (1 << 17); ++w)
-      if (stamps[w * 8 + 0]) x.push_back((double)stamps[w * 8 + s]);
+      if (stamps[w * 8 + 6]) x.push_back((double)stamps[w * 8 + s]);
     if (x.empty()) continue;
     std::sort(x.begin(), x.end());
     const double med = x[x.size() / 2];
