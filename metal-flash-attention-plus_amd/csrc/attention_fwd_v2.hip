@@ -484,6 +484,63 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   int a0, a1, b0, b1;
   key_range(p, rbA * BQ, BQ, BK, &a0, &a1);
   key_range(p, MIRROR ? rbB * BQ : rbA * BQ, BQ, BK, &b0, &b1);
+  // Sparse ranges (adjacent pairs; SparseMQABuilder.swift:30-62, AttentionKernel+Softmax.swift:
+  // 278-304): each row's keys [x, y).  The pair stages the tiles between the first and last key
+  // any of its 256 rows keeps; a group computes only the tiles that meet its own block's union,
+  // masks with its rows' ranges (no mask on tiles inside every range of the block), and rows
+  // left with no unmasked key are written after the loop (fill_masked_rows).
+  int rlo = -0x40000000, rhi = 0x3fffffff, in_lo = 0, in_hi = 0x3fffffff;
+  int g_lo = 0, g_hi = 0x3fffffff;  // this group's block union
+  bool row_empty = false;
+  if (!MIRROR && p.mask.ranges) {
+    const int qr = (g == 0 ? rbA : rbB) * BQ + wg * 32 + l32;
+    uint32_t x = 0u, y = 0u;
+    if (qr < p.R) {
+      const uint32_t* rp = p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + qr);
+      x = rp[0];
+      y = rp[1];
+      row_empty = masked_everywhere(p, x, y, qr);
+    }
+    rlo = (int)min(x, 0x3fffffffu);
+    rhi = (int)min(y, 0x3fffffffu) - 1;
+    const bool ne = x < y;
+    int mn = ne ? rlo : 0x3fffffff, mx = ne ? rhi + 1 : 0;
+    in_lo = ne ? rlo : 0;
+    in_hi = ne ? rhi + 1 : 0x3fffffff;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mn = min(mn, __shfl_xor(mn, o));
+      mx = max(mx, __shfl_xor(mx, o));
+      in_lo = max(in_lo, __shfl_xor(in_lo, o));
+      in_hi = min(in_hi, __shfl_xor(in_hi, o));
+    }
+    int* red = reinterpret_cast<int*>(smem);
+    if (lane == 0) {
+      const int wv = tid >> 6;
+      red[4 * wv] = mn;
+      red[4 * wv + 1] = mx;
+      red[4 * wv + 2] = in_lo;
+      red[4 * wv + 3] = in_hi;
+    }
+    __syncthreads();
+    int umn = 0x3fffffff, umx = 0;
+    g_lo = 0x3fffffff;
+    g_hi = 0;
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) {
+      umn = min(umn, red[4 * w8]);
+      umx = max(umx, red[4 * w8 + 1]);
+      if (w8 / 4 == g) {
+        g_lo = min(g_lo, red[4 * w8]);
+        g_hi = max(g_hi, red[4 * w8 + 1]);
+        in_lo = max(in_lo, red[4 * w8 + 2]);
+        in_hi = min(in_hi, red[4 * w8 + 3]);
+      }
+    }
+    __syncthreads();  // the reduction slots are the first K slot's bytes
+    b0 = max(b0, (umn / BK) * BK);
+    b1 = min(b1, umx);
+  }
   const int nB = b1 > b0 ? (b1 - b0 + BK - 1) / BK : 0;
   // Mirrored: the odd middle block is B only.
   const int nA = !MIRROR ? nB : rbA < rbB && a1 > a0 ? (a1 - a0 + BK - 1) / BK : 0;
@@ -498,7 +555,7 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     return s < S && i < nB;
   };
 
-  int q0 = (g == 0 && nA > 0 ? rbA : rbB) * BQ;
+  int q0 = (g == 0 && (nA > 0 || !MIRROR) ? rbA : rbB) * BQ;
   int qi = q0 + wg * 32 + l32;
   i16x8 qf[DP / 16];
   DmaA<DP, 32, 64> qd;  // this wave's 32 Q rows (group 0: B's, staged for the switch)
@@ -629,11 +686,13 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
       st.init();
     }
     int tc;
-    if (tile(s, tc)) {
+    // (Sparse ranges: a group skips the tiles outside its block's union.)
+    if (tile(s, tc) && tc + BK > g_lo && tc < g_hi) {
       const bool shared = s < nA;
       const char* kt = (shared ? sk : kb0) + (s & 1) * TILEB;
       const char* vt = (shared ? sv : vb0) + (s & 1) * TILEB;
-      const bool mask_tile = (tc + BK > p.C) || (p.mask.causal && tc + BK - 1 > q0);
+      const bool mask_tile = (tc + BK > p.C) || (p.mask.causal && tc + BK - 1 > q0) ||
+                             tc < in_lo || tc + BK > in_hi;
       if constexpr (FIRST) {
         // V0 is older than the next shared tile's pieces issued above.
         constexpr int NPN = 2 * DmaA<DP, BK, 2 * NT>::PPW;
@@ -645,7 +704,8 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
         __syncthreads();
         fwd2_pv<E, DP, BK>(vt, trb, pb, st);
       } else {
-        fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh);
+        fwd2_tile<E, DP, BK>(kt, vt, rbase, trb, qf, st, tc, mask_tile, qi, p, c, wsz, hh,
+                             NoHook(), rlo, rhi);
       }
     }
     if (sw && full_sw)
@@ -696,9 +756,21 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
         store_o_image<DP, 128, 2 * NT, NTS>(p, obase, smem + blk * 128 * ORS, ORS, qb, tid,
                                             qb + BQ <= p.R && p.D == DP);
       }
+      if (p.mask.ranges) {
+        // Rows with no unmasked key: the image wrote them from an empty state; the owning wave
+        // rewrites them once every store of the workgroup has completed.
+        const uint64_t todo = __ballot(row_empty && hh == 0);
+        wait_vm();
+        __syncthreads();
+        if (todo) fill_masked_rows<E, DP>(p, b, h, kvh, q0 + wg * 32, todo, lane);
+      }
       return;
     }
-    if (qi < p.R && (g == 1 || nA > 0)) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+    if (qi < p.R && (g == 1 || nA > 0) && !row_empty) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+    if (p.mask.ranges) {
+      const uint64_t todo = __ballot(row_empty && hh == 0);
+      if (todo) fill_masked_rows<E, DP>(p, b, h, kvh, q0 + wg * 32, todo, lane);
+    }
     return;
   }
   // Merge group 1's partial state of B into group 0 through LDS.
@@ -864,7 +936,10 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   // any size (tests).
   const char* sv = getenv("MFA_FWD_SHARE");
   // (An odd block count leaves group 1 of the last pair without rows: not for nblk < 8 odd.)
-  const bool adj = !p.mask.causal && !p.mask.window && !p.mask.ranges && !var &&
+  // Sparse ranges take the adjacent pairs too (D <= 128): the pair stages the union of its
+  // blocks' key ranges and each group computes its own (MFA_FWD_SHARE=0 keeps the single-block
+  // kernel with tile skipping).
+  const bool adj = !p.mask.causal && !p.mask.window && (!p.mask.ranges || DP <= 128) && !var &&
                    (sv ? sv[0] == '1'
                        : (p.nblk % 2 == 0 || p.nblk >= 8) &&
                              (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);

@@ -120,3 +120,75 @@ def test_mostly_empty_rows(gpu, D):
     K, V = gaussian((B, Hkv, C, D), 931), gaussian((B, Hkv, C, D), 932)
     plan = check(Q, K, V, FP16, ranges)
     assert len(plan) == 1 and "mfa_fwd2_kernel" in plan[0], plan
+
+
+# --------------------------------------------------------------- ranges on the shared tiles
+# Adjacent pairs of 128-row blocks share every staged tile (attention_fwd_v2.hip, the
+# shared-tile kernel): with ranges the pair stages the union of its blocks' key ranges and each
+# group computes and masks only its own.  MFA_FWD_SHARE=1 takes that kernel at any size.
+@pytest.mark.parametrize("prec", [FP16, BF16])
+@pytest.mark.parametrize("D", [64, 128])
+def test_block_sparse_shared_tiles(gpu, prec, D, monkeypatch):
+    monkeypatch.setenv("MFA_FWD_SHARE", "1")
+    B, H, Hkv, S, blk = 1, 4, 2, 1000, 64
+    nb = (S + blk - 1) // blk
+    ranges = np.stack([block_ranges(banded_pattern(nb, nb, 3, 940 + kv, empty_every=5), blk, S, S)
+                       for kv in range(Hkv)])[None]
+    Q = gaussian((B, H, S, D), 941)
+    K, V = gaussian((B, Hkv, S, D), 942), gaussian((B, Hkv, S, D), 943)
+    plan = check(Q, K, V, prec, ranges)
+    assert len(plan) == 1 and plan[0].startswith("mfa_fwd2_share_kernel") and ", false" in plan[0], plan
+
+
+def test_block_sparse_shared_disjoint_blocks(gpu, monkeypatch):
+    """The two blocks of a pair keep disjoint key ranges (the first block the first 300 keys, the
+    second the last 300), with empty and narrowed single rows and an odd block count: each group
+    must compute only its own tiles of the staged union."""
+    monkeypatch.setenv("MFA_FWD_SHARE", "1")
+    B, H, R, C, D = 2, 2, 5 * 128 + 40, 1100, 128
+    ranges = np.zeros((B, H, R, 2), dtype=np.uint32)
+    blk = np.arange(R) // 128
+    ranges[..., 0] = np.where(blk % 2 == 0, 0, C - 300)[None, None]
+    ranges[..., 1] = np.where(blk % 2 == 0, 300, C)[None, None]
+    ranges[0, 0, 7::23, 1] = ranges[0, 0, 7::23, 0]            # empty rows
+    ranges[1, 1, 11::17, 0] = ranges[1, 1, 11::17, 0] + 90      # narrowed rows
+    Q = gaussian((B, H, R, D), 951)
+    K, V = gaussian((B, H, C, D), 952), gaussian((B, H, C, D), 953)
+    plan = check(Q, K, V, FP16, ranges)
+    assert plan[0].startswith("mfa_fwd2_share_kernel"), plan
+
+
+def test_mostly_empty_rows_shared_tiles(gpu, monkeypatch):
+    monkeypatch.setenv("MFA_FWD_SHARE", "1")
+    B, H, Hkv, R, C, blk = 1, 2, 2, 512, 2048, 64
+    nqb, nkb = R // blk, C // blk
+    pat = np.zeros((nqb, nkb), dtype=np.uint8)
+    pat[::4, : nkb // 2] = 1
+    ranges = np.stack([block_ranges(pat, blk, R, C) for _ in range(Hkv)])[None]
+    Q = gaussian((B, H, R, 128), 960)
+    K, V = gaussian((B, Hkv, C, 128), 961), gaussian((B, Hkv, C, 128), 962)
+    plan = check(Q, K, V, BF16, ranges)
+    assert plan[0].startswith("mfa_fwd2_share_kernel"), plan
+
+
+def test_block_sparse_bench_shape_routes_shared(gpu):
+    """The bench's block-sparse row (B1 H16 S4096 D128, band of 8 of 32 key blocks) takes the
+    shared-tile kernel by default; heads 0 and 15 against the oracle."""
+    B, H, S, D, blk = 1, 16, 4096, 128, 128
+    nb = S // blk
+    pat = np.zeros((nb, nb), dtype=np.uint8)
+    for i in range(nb):
+        lo = min(max(0, i - 4), nb - 8)
+        pat[i, lo:lo + 8] = 1
+    ranges = np.stack([block_ranges(pat, blk, S, S) for _ in range(H)])[None]
+    g = np.random.default_rng(970)
+    Q, K, V = (g.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
+    mfa.last_launches()
+    o, l = run_forward(Q, K, V, prec=FP16, ranges=ranges, low_precision_intermediates=False)
+    plan = [x["name"] for x in mfa.last_launches()]
+    assert plan[0].startswith("mfa_fwd2_share_kernel") and ", false" in plan[0], plan
+    for hh in (0, 15):
+        sub = lambda x: np.ascontiguousarray(x[:, hh:hh + 1])
+        ref = ol.attention(seen(sub(Q), FP16), seen(sub(K), FP16), seen(sub(V), FP16),
+                           ranges=np.ascontiguousarray(ranges[:, hh:hh + 1]))
+        assert maxerr(o[:, hh:hh + 1].cpu().numpy(), ref["O"]) <= 5e-3

@@ -2,7 +2,8 @@
 
 Usage: python tools/ab_env.py WORKLOAD VAR=a,b,c [VAR2=x,y] — times each setting by HIP
 events (median of 5 rounds of 20 launches), interleaving settings round by round.
-WORKLOAD: c3_int8_exact | c3_fp16 | c2
+WORKLOAD: c3_int8_exact | c3_fp16 | c2 | sparse (the bench's block-sparse row).  A value "-"
+unsets the variable (the library default).
 """
 import itertools
 import os
@@ -49,6 +50,27 @@ def workload(name, dev="cuda:0"):
         desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
         return (lambda: mfa.MultiHeadAttention().forward(desc, q, k, v, o, l, stream=stream)), \
             mfa.attention_flops(B, H, S, S, D, causal=True)
+    if name == "sparse":
+        import numpy as np
+        B, H, S, D, blk, band = 1, 16, 4096, 128, 128, 8
+        nb = S // blk
+        pat = np.zeros((nb, nb), dtype=np.uint8)
+        for i in range(nb):
+            c0 = min(max(0, i - band // 2), nb - band)
+            pat[i, c0:c0 + band] = 1
+        rb = np.zeros((nb, 2), dtype=np.uint32)
+        mfa.lib.mfa_sparse_build_block_sparse(pat.ctypes.data, nb, nb, blk, rb.ctypes.data)
+        rows = np.ascontiguousarray(np.broadcast_to(np.repeat(rb, blk, axis=0), (B, H, S, 2)))
+        mask = torch.from_numpy(rows.view(np.int32)).to(dev)
+        q, k, v = (u((B, H, S, D), torch.float16) for _ in range(3))
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.FP16,
+                                            sparse_mask=mfa.MaskType.sparseRanges)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+        pairs = int((rows[0, 0, :, 1].astype(np.int64) - rows[0, 0, :, 0]).sum()) * B * H
+        return (lambda: mfa.MultiHeadAttention().forward(desc, q, k, v, o, l, mask=mask,
+                                                         stream=stream)), 4.0 * D * pairs
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -67,7 +89,10 @@ def main():
     for _ in range(5):
         for s in settings:
             for k, v in s:
-                os.environ[k] = v
+                if v == "-":
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
             for _ in range(5):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
