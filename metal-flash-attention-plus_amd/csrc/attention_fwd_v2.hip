@@ -461,8 +461,12 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   char* const qstg = smem + 8 * TILEB + wg * QW;
 
   const int BH = p.B * p.H;
-  const int pi = blockIdx.x / BH;
-  const int bh = blockIdx.x % BH;
+  int pi = blockIdx.x / BH;
+  int bh = blockIdx.x % BH;
+  // Adjacent (unmasked) pairs: each XCD walks one head's pairs at a time (xcd_unit_block), so
+  // the K/V of the heads in flight on an XCD stay in its 4 MiB L2 (a head's K/V is 4 MiB at
+  // S 8192 D 128 and at S 4096 D 256); dealt round-robin, an XCD held 2-8 heads at once.
+  if (!MIRROR && p.xcd_heads) xcd_unit_block(blockIdx.x, BH, (p.nblk + 1) / 2, &bh, &pi);
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const float c = p.c_log2;
   const int wsz = 0x3fffffff;
@@ -836,6 +840,10 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   FwdParams q = p;
   q.nblk = (p.R + 127) / 128;
   const int npairs = (q.nblk + 1) / 2;
+  {
+    const char* xh = getenv("MFA_SHARE_XCD");  // A/B: 0 deals pairs round-robin over heads
+    q.xcd_heads = !(xh && xh[0] == '0');
+  }
   // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
   // (A/B).
   // Mirrored pairs: deferred V0 (+1.2 % at C2 in one-process A/B) and non-temporal O image

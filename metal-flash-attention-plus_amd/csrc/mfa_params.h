@@ -49,6 +49,7 @@ struct FwdParams {
   void* ws;
   int32_t sk_len, sk_total, sk_head, sk_cnt_bytes;
   int32_t sk_flags;        // bit 0: closers always publish (tests)
+  int32_t xcd_heads;       // adjacent shared-tile pairs: a head's pairs together on one XCD
 };
 
 struct BwdParams {
