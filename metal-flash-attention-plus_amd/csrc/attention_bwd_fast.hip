@@ -337,7 +337,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
 // ---------------------------------------------------------------------------------------
 // backwardKeyValue.  Grid: nblk x B x H_kv (first key blocks carry the most causal query
 // tiles).  128 keys per workgroup; BQ query rows per step.
-template <class E, int DP, int BQ>
+// KVQ: K/V storage — SRC_SAME (16-bit), or SRC_I8 / SRC_I4 per-tensor quantised (a separate
+// instantiation, so the 16-bit kernel's register allocation is untouched).
+template <class E, int DP, int BQ, int KVQ = SRC_SAME>
 __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   using A = Arith16<E, DP>;
   constexpr int NT = 256, BK = 128, NJ = BQ / 32, DS = DP / 16, ND = DP / 32;
@@ -363,10 +365,30 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   i16x8 kf[DS], vf[DS];
   {
     const int kk = kvalid ? ki : 0;
-    load_frags16<DP>(kf, (const uint16_t*)p.k.ptr + (int64_t)b * p.k.sb +
-                             (int64_t)kvh * p.k.sh + (int64_t)kk * p.k.ss, kvalid, p.D, hh);
-    load_frags16<DP>(vf, (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb +
-                             (int64_t)kvh * p.v.sh + (int64_t)kk * p.v.ss, kvalid, p.D, hh);
+    if constexpr (KVQ != SRC_SAME) {
+      // Quantised per-tensor K/V (QuantizedAttention.backwardKeyValue): the key block's rows
+      // are read once per workgroup, so they are widened here, in registers, to exactly the
+      // operands the dequantisation pass would have written (the integers q - zp; the scales
+      // stay folded) — no pass, no dense copy, bit-identical results.
+      auto qload = [&](i16x8 (&f)[DS], const Operand& op) {
+        const int64_t rowoff = (int64_t)b * op.sb + (int64_t)kvh * op.sh + (int64_t)kk * op.ss;
+        const float zp = (float)op.zp;
+#pragma unroll
+        for (int sidx = 0; sidx < DS; ++sidx) {
+          const int d0 = 16 * sidx + 8 * hh;
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (kvalid && d0 < p.D) v = dequant_fast<E, KVQ>(load_qchunk<KVQ>(op, rowoff, d0, p.D), zp);
+          f[sidx] = __builtin_bit_cast(i16x8, v);
+        }
+      };
+      qload(kf, p.k);
+      qload(vf, p.v);
+    } else {
+      load_frags16<DP>(kf, (const uint16_t*)p.k.ptr + (int64_t)b * p.k.sb +
+                               (int64_t)kvh * p.k.sh + (int64_t)kk * p.k.ss, kvalid, p.D, hh);
+      load_frags16<DP>(vf, (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb +
+                               (int64_t)kvh * p.v.sh + (int64_t)kk * p.v.ss, kvalid, p.D, hh);
+    }
   }
 
   int qbeg = 0, qend = p.R;
@@ -687,10 +709,12 @@ template <class E, int DP>
 static hipError_t launch_bwd_kv_fast(const BwdParams& p, hipStream_t stream) {
   constexpr int BQ = BwdFastCfg<DP>::BQ;
   constexpr int LDS = 4 * BQ * DP * 2 + 4 * BQ * 4;
-  auto kern = mfa_bwd_kv_fast_kernel<E, DP, BQ>;
   BwdParams q = p;
   q.nblk = (p.C + 127) / 128;
-  return launch(kern, dim3(q.nblk * p.B * p.Hkv), dim3(256), LDS, stream, q);
+  const dim3 grid(q.nblk * p.B * p.Hkv);
+  if (p.k.prec == P_INT8) return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ, SRC_I8>, grid, dim3(256), LDS, stream, q);
+  if (p.k.prec == P_INT4) return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ, SRC_I4>, grid, dim3(256), LDS, stream, q);
+  return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ>, grid, dim3(256), LDS, stream, q);
 }
 
 // kind: 0 = backwardQuery, 1 = backwardKeyValue.  hipErrorNotSupported when not covered.
@@ -716,7 +740,9 @@ hipError_t bwd_fast_dispatch(const BwdParams& p, int kind, int elem, int DP, hip
 namespace mfa {
 #define MFA_BF_INST(EE, DPV)                                                                   \
   template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT>(BwdParams);   \
-  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ>(BwdParams);
+  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ>(BwdParams);    \
+  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I8>(BwdParams); \
+  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I4>(BwdParams);
 MFA_BF_INST(F16, 64)
 MFA_BF_INST(F16, 128)
 MFA_BF_INST(F16, 256)

@@ -1057,15 +1057,24 @@ enum BwdPhase { PHASE_QUERY = 1, PHASE_KV = 2, PHASE_BOTH = 3 };
 
 // The tuned backward kernels (attention_bwd_fast.hip) cover 16-bit Q/K/V/dO with contiguous
 // 16-byte aligned rows, D % 8 == 0, and no mask or skippable causal / window masks.
-bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int qsrc) {
+// kv_quant: the backwardKeyValue kernel, which reads K and V once per workgroup into
+// registers, takes per-tensor quantised K/V (INT8/INT4, dense rows) directly.
+bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int qsrc,
+                       bool kv_quant = false) {
   if (const char* e = getenv("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return false;
   }
   if (elem != 1 && elem != 2) return false;
   if (DP != 64 && DP != 128 && DP != 256) return false;
-  if (ksrc != 0 || qsrc != 0 || p.D % 8 != 0) return false;
+  if (qsrc != 0 || p.D % 8 != 0) return false;
+  if (ksrc != 0 && !kv_quant) return false;
   const int prec = elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16;
   for (const mfa::Operand* op : {&p.q, &p.k, &p.v, &p.dO_op}) {
+    const bool kvq = ksrc != 0 && (op == &p.k || op == &p.v);
+    if (kvq) {
+      if (!is_quantized(op->prec) || op->sd != 1 || op->bscale) return false;
+      continue;
+    }
     if (op->prec != prec || !op->vec || op->sd != 1 || op->bscale) return false;
   }
   if (p.mask.amask || p.mask.ranges) return false;
@@ -1074,7 +1083,7 @@ bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int 
   if (p.o_sd != 1 || p.dq_sd != 1 || p.dk_sd != 1 || p.dv_sd != 1) return false;
   // Tiles are addressed per head with 32-bit buffer offsets.
   const int64_t lim = (int64_t)1 << 31;
-  if ((int64_t)p.C * p.k.ss * 2 >= lim || (int64_t)p.C * p.v.ss * 2 >= lim ||
+  if ((ksrc == 0 && ((int64_t)p.C * p.k.ss * 2 >= lim || (int64_t)p.C * p.v.ss * 2 >= lim)) ||
       (int64_t)p.R * p.q.ss * 2 >= lim || (int64_t)p.R * p.dO_op.ss * 2 >= lim)
     return false;
   return true;
@@ -1107,9 +1116,12 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
   if (phase & PHASE_KV) {
     p.nblk = (p.C + bp - 1) / bp;
     if (p.C > 0) {
-      hipError_t e = big    ? mfa::bwd_bigd_dispatch(p, 1, elem, stream)
-                     : fast ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream)
-                            : hipErrorNotSupported;
+      // Quantised K/V with 16-bit Q reach here only for backwardKeyValue alone (see
+      // quantized_backward): its fast kernel widens them in registers.
+      const bool fast_kv = fast || (!big && ksrc > 0 && bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true));
+      hipError_t e = big       ? mfa::bwd_bigd_dispatch(p, 1, elem, stream)
+                     : fast_kv ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream)
+                               : hipErrorNotSupported;
       if (big && e == hipErrorNotSupported)
         return fail(MFA_ERR_UNSUPPORTED, "head dimension %d: mixed operand precisions", p.D);
       if (e == hipErrorNotSupported) e = mfa::bwd_kv_dispatch(p, elem, DP, ksrc, qsrc, stream);
@@ -1269,7 +1281,14 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   p.dk_mul = fq;
   if ((st = plan_masks(base, nullptr, R, C, &p.mask)) != MFA_SUCCESS) return st;
   int ksrc = src_kind(kp), qsrc = src_kind(qp);
-  if (dequant_pass_worth(R, H, Hkv, D, elem)) {
+  // backwardKeyValue alone with 16-bit Q: its kernel reads each key block's K/V rows once per
+  // workgroup into registers and widens them there, so the pass would only add traffic
+  // (MFA_KV_REGS=0 keeps the pass: A/B, bit-identity tests).
+  const char* kvr = getenv("MFA_KV_REGS");
+  const bool kv_regs = phase == PHASE_KV && ksrc > 0 && qsrc == 0 && !(kvr && kvr[0] == '0') &&
+                       !dequant_pass_needed(D) &&
+                       bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true);
+  if (dequant_pass_worth(R, H, Hkv, D, elem) && !kv_regs) {
     hipStream_t s = (hipStream_t)stream;
     if (ksrc > 0) {
       if ((st = dequant_copy(&p.k, B, Hkv, C, D, elem, 6, s)) != MFA_SUCCESS) return st;

@@ -385,12 +385,13 @@ def test_dequant_pass_backward_on_fast_kernels(gpu, kv):
     plan = (mfa.quantized_plan(desc, mfa.KernelType.backwardQuery, tq, tk, tv) +
             mfa.quantized_plan(desc, mfa.KernelType.backwardKeyValue, tq, tk, tv))
     assert plan[2]["name"].startswith("mfa_bwd_q_fast_kernel<F16, 128")
-    assert plan[5]["name"].startswith("mfa_bwd_kv_fast_kernel<F16, 128")
+    # backwardKeyValue widens the quantised K/V in the kernel's registers: no pass.
+    assert len(plan) == 4 and plan[3]["name"].startswith("mfa_bwd_kv_fast_kernel<F16, 128"), plan
     mfa.last_launches()
     qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
     qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
     torch.cuda.synchronize()
-    assert mfa.last_launches() == plan[2:]  # the log keeps the last four launches
+    assert mfa.last_launches() == plan  # the log keeps the last four launches
     for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
         assert maxerr(t, ref[name]) < 5e-2, name
 
@@ -775,3 +776,59 @@ def test_forward_from_float_buffers_wraps_unquantized_target(gpu):
     torch.cuda.synchronize()
     ref = ol.attention(*(t.float().cpu().numpy() for t in (q, k, v)))["O"]
     assert maxerr(o1, ref) < 5e-3
+
+
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("D,causal,Hkv,zps,prec", [(128, True, 2, (0, 0), P.FP16),
+                                                   (64, False, 4, (3, -2), P.BF16),
+                                                   (256, False, 1, (0, 0), P.FP16),
+                                                   (256, True, 2, (-5, 4), P.BF16)])
+def test_backward_key_value_widens_in_registers(gpu, kv, D, causal, Hkv, zps, prec, monkeypatch):
+    """backwardKeyValue alone with 16-bit Q/dO reads per-tensor INT8/INT4 K/V straight into the
+    tuned kernel's registers (no dequantisation pass): dK and dV are bit-identical to the pass
+    path (MFA_KV_REGS=0), and match the oracle on the dequantised values."""
+    B, H, S = 1, 4, 320
+    rng = np.random.default_rng(D + 7 * Hkv)
+    Q, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) * 0.5 for _ in range(2))
+    K, V = (rng.standard_normal((B, Hkv, S, D)).astype(np.float32) * 0.5 for _ in range(2))
+    kq, ks, kd = quantize_host(K, kv)
+    vq, vs, vd = quantize_host(V, kv)
+    kz, vz = zps
+    if kv == P.INT4:
+        kz, vz = max(-7, min(7, kz)), max(-7, min(7, vz))
+    base = mfa.AttentionDescriptor.make(S, S, D, causal=causal, low_precision=True, precision=prec)
+    desc = mfa.quantized_descriptor(base, prec, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, prec), prec)
+    tk = mfa.quantized_tensor(tdev(kq, torch.uint8), kv, scale=ks, zero_point=kz)
+    tv = mfa.quantized_tensor(tdev(vq, torch.uint8), kv, scale=vs, zero_point=vz)
+    # The reference of the zero-point-shifted tensors: (q - zp) * s.
+    kd = ol.dequantize(kq, K.size, int(kv), ks, kz).reshape(K.shape) if kz else kd
+    vd = ol.dequantize(vq, V.size, int(kv), vs, vz).reshape(V.shape) if vz else vd
+    Qd, dOd = seen(Q, prec), seen(dO, prec)
+    # Query head h reads kv head h % Hkv (MultiHeadAttention broadcast).
+    ref = ol.attention(Qd, np.tile(kd, (1, H // Hkv, 1, 1)), np.tile(vd, (1, H // Hkv, 1, 1)),
+                       dO=dOd, causal=causal)
+    o = tdev(ref["O"])
+    l = torch.from_numpy(ref["L"]).half().to(DEV)
+    do = to_device(dO, prec)
+    dvals = torch.empty((B, H, S), dtype=torch.bfloat16, device=DEV)
+    qa = mfa.QuantizedAttention()
+    dq = torch.empty((B, H, S, D), dtype=torch.float32, device=DEV)
+    qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MFA_KV_REGS", mode)
+        dk = torch.full((B, Hkv, S, D), float("nan"), dtype=torch.float32, device=DEV)
+        dv = torch.full_like(dk, float("nan"))
+        mfa.last_launches()
+        qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
+        torch.cuda.synchronize()
+        outs[mode] = (dk, dv, [r["name"] for r in mfa.last_launches()])
+    names = outs["1"][2]
+    assert not any("dequant" in n for n in names), names
+    assert names[-1].startswith("mfa_bwd_kv_fast_kernel<"), names
+    assert any("dequant" in n for n in outs["0"][2]), outs["0"][2]
+    assert torch.equal(outs["0"][0], outs["1"][0]) and torch.equal(outs["0"][1], outs["1"][1])
+    gk = ref["dK"].reshape(B, H // Hkv, Hkv, S, D).sum(axis=1)
+    gv = ref["dV"].reshape(B, H // Hkv, Hkv, S, D).sum(axis=1)
+    assert maxerr(outs["1"][0], gk) < 5e-2 and maxerr(outs["1"][1], gv) < 5e-2
