@@ -1,9 +1,12 @@
 // attention_bwd_fast.hip — the two phases of the reference's 7-GEMM backward, tuned for the
 // common case on gfx950: fp16/bf16 Q/K/V/dO with 16-byte aligned contiguous rows, D % 8 == 0,
 // D <= DP ∈ {64, 128, 256}, no mask or causal / sliding-window masks whose fully masked tiles
-// may be skipped (no additive mask, no sparse ranges).  Same algorithm and numerics contract as
-// attention_bwd.h (AttentionKernel+Source.swift:418-511, Softmax.swift:31-236 / :795-804);
-// everything else goes to that generic kernel.
+// may be skipped.  Same algorithm and numerics contract as attention_bwd.h
+// (AttentionKernel+Source.swift:418-511, Softmax.swift:31-236 / :795-804); everything else goes
+// to that generic kernel.  Additive masks and sparse ranges run a separate instantiation
+// (MSK = true) that applies every mask element by element on every tile, skips nothing unless
+// skip_ok, and takes the exact-product path for rows at the mask level (fully masked rows),
+// as the generic kernel does; the unmasked instantiations are untouched by it.
 //
 // Structure (both phases): 4 waves, one per SIMD (up to 512 registers per lane), 32 rows per
 // wave held in registers for the whole kernel; the traversed operand pair streams through a
@@ -164,7 +167,7 @@ __device__ __forceinline__ void tr_chain(const char* tile, const int (&trb)[2], 
 
 // ---------------------------------------------------------------------------------------
 // backwardQuery.  Grid: nblk x B x H, heaviest causal blocks first.  BT keys per tile.
-template <class E, int DP, int BT>
+template <class E, int DP, int BT, bool MSK = false>
 __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   using A = Arith16<E, DP>;
   constexpr int NT = 256, BQ = 128, NJ = BT / 32, DS = DP / 16, ND = DP / 32;
@@ -204,6 +207,56 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   if (p.mask.window && p.mask.skip_ok) {
     const int64_t lo = (int64_t)q0 - (int64_t)p.mask.window_size;
     kbeg = lo > 0 ? (int)(lo / BT) * BT : 0;
+  }
+  // MSK: ranges, causal and window each leave an interval of keys, so a row's unmasked keys are
+  // one interval [elo, ehi); a row with none (elo >= ehi, stored as [C, 0)) is masked
+  // everywhere and sits at the mask level, where every key counts (uniform P).  Unless the block
+  // holds such a row, its key tiles run over the union of its rows' intervals only (the others
+  // give P = 0 exactly); tiles inside every row's interval need no per-element mask.
+  int elo = 0, ehi = p.C, tin_lo = 0, tin_hi = p.C;
+  if constexpr (MSK) {
+    int64_t lo = 0, hi = p.C;
+    if (p.mask.ranges && qvalid) {
+      const uint32_t* rp = p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + qi);
+      lo = rp[0];
+      hi = min((int64_t)rp[1], (int64_t)p.C);
+    }
+    if (p.mask.causal) hi = min(hi, (int64_t)qi + 1);
+    if (p.mask.window) lo = max(lo, (int64_t)qi - (int64_t)p.mask.window_size);
+    const bool empty = qvalid && lo >= hi;
+    elo = empty ? p.C : (int)lo;
+    ehi = empty ? 0 : (int)hi;
+    // Block reductions over valid rows: union [umn, umx) of the non-empty rows, intersection
+    // [tin_lo, tin_hi) of all rows, and whether any row is empty.
+    int umn = qvalid && !empty ? elo : p.C, umx = qvalid && !empty ? ehi : 0;
+    int imx = qvalid ? elo : 0, imn = qvalid ? ehi : p.C;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      umn = min(umn, __shfl_xor(umn, o));
+      umx = max(umx, __shfl_xor(umx, o));
+      imx = max(imx, __shfl_xor(imx, o));
+      imn = min(imn, __shfl_xor(imn, o));
+    }
+    const bool wempty = __ballot(empty) != 0;
+    int* red = reinterpret_cast<int*>(smem + 4 * TILEB);
+    if (lane == 0) {
+      red[wave * 5] = umn; red[wave * 5 + 1] = umx; red[wave * 5 + 2] = imx;
+      red[wave * 5 + 3] = imn; red[wave * 5 + 4] = wempty;
+    }
+    __syncthreads();
+    bool any_empty = false;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      umn = min(umn, red[w * 5]); umx = max(umx, red[w * 5 + 1]);
+      imx = max(imx, red[w * 5 + 2]); imn = min(imn, red[w * 5 + 3]);
+      any_empty = any_empty || red[w * 5 + 4];
+    }
+    if (!any_empty) {
+      kbeg = max(kbeg, (umn / BT) * BT);
+      kend = min(kend, umx);
+    }
+    tin_lo = imx;
+    tin_hi = imn;
   }
   DmaA<DP, BT, NT> kd, vd;
   kd.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
@@ -246,6 +299,12 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   }
   const float c = p.c_log2, sc = p.scale;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+  // MSK: a row at the mask level (every key masked) takes the rounded product S·c before
+  // subtracting L, as the generic kernel does (attention_bwd.h).
+  const bool lmask = MSK && Lrow < kMaskLevel;
+  auto pexp = [&](float x) {
+    return __builtin_amdgcn_exp2f(lmask ? mul_rn(x, c) - Lrow : __builtin_fmaf(x, c, -Lrow));
+  };
 
   f32x16 dq[ND];
 #pragma unroll
@@ -267,8 +326,37 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     f32x16 s[NJ], dp[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) { s[j] = zero16(); dp[j] = zero16(); }
+    // MSK: this tile's additive-mask values, issued before the S chain so it hides them;
+    // element (j, i) is key t + 32j + 8(i>>2) + 4hh + (i&3) of this lane's row.
+    float am[MSK ? NJ : 1][16];
+    if constexpr (MSK) {
+      const float* arow = p.mask.amask + row * p.C;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = t + 32 * j + 8 * (i >> 2) + 4 * hh + (i & 3);
+          am[j][i] = (p.mask.amask && qvalid && key < p.C) ? arow[key] : 0.f;
+        }
+    }
     rows_chain<A, NJ>(kt, qf, s, rbase, [](int) {});
-    const bool diag = (p.mask.causal && t + BT - 1 > q0) || p.mask.window;
+    if constexpr (MSK) {
+      if (t >= tin_lo && min(t + BT, p.C) <= tin_hi) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[j][i] += am[j][i];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = t + 32 * j + 8 * (i >> 2) + 4 * hh + (i & 3);
+            s[j][i] = (key < elo || key >= ehi) ? kMaskValue : s[j][i] + am[j][i];
+          }
+      }
+    }
+    const bool diag = !MSK && ((p.mask.causal && t + BT - 1 > q0) || p.mask.window);
     if (diag) {
       MFA_KEEP_BRANCH();
       {
@@ -284,7 +372,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
 #pragma unroll
         for (int e = 0; e < EPM; ++e) {
           const int idx = i * EPM + e, jj = idx >> 4, ii = idx & 15;
-          s[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -Lrow));
+          s[jj][ii] = pexp(s[jj][ii]);
         }
       });
     }
@@ -339,7 +427,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
 // tiles).  128 keys per workgroup; BQ query rows per step.
 // KVQ: K/V storage — SRC_SAME (16-bit), or SRC_I8 / SRC_I4 per-tensor quantised (a separate
 // instantiation, so the 16-bit kernel's register allocation is untouched).
-template <class E, int DP, int BQ, int KVQ = SRC_SAME>
+template <class E, int DP, int BQ, int KVQ = SRC_SAME, bool MSK = false>
 __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   using A = Arith16<E, DP>;
   constexpr int NT = 256, BK = 128, NJ = BQ / 32, DS = DP / 16, ND = DP / 32;
@@ -349,6 +437,10 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   char* const ob0 = smem + 2 * TILEB;
   float* const lb0 = reinterpret_cast<float*>(smem + 4 * TILEB);  // [2][BQ] L, then [2][BQ] D
   float* const db0 = lb0 + 2 * BQ;
+  // MSK: [2][BQ] unmasked key interval per row, [2][BQ][BK] additive mask, [2] step flags.
+  int2* const rg0 = reinterpret_cast<int2*>(db0 + 2 * BQ);
+  float* const am0 = reinterpret_cast<float*>(rg0 + 2 * BQ);
+  int* const fl0 = reinterpret_cast<int*>(am0 + 2 * BQ * 128);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -415,6 +507,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   // The loads leave raw bits in registers and are converted only at the step's end, so their
   // latency hides under the step (a conversion right after the load waits for it).
   uint32_t lraw = 0u, draw = 0u;
+  uint2 rraw = make_uint2(0u, 0xffffffffu);
   bool ldv = false;
   auto ld_load = [&](int h, int t) {
     if (tid < BQ) {
@@ -425,14 +518,60 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
                      : reinterpret_cast<const uint32_t*>(p.l)[r];
       draw = p.d_bf16 ? (uint32_t)reinterpret_cast<const uint16_t*>(p.dD)[r]
                       : reinterpret_cast<const uint32_t*>(p.dD)[r];
+      if (MSK && p.mask.ranges)  // ranges are per kv head: [B, H_kv, R, 2]
+        rraw = *reinterpret_cast<const uint2*>(
+            p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + (ldv ? q : 0)));
     }
   };
-  auto ld_store = [&](int buf) {
+  // MSK: ranges, causal and window each leave an interval of keys, so row q's unmasked keys
+  // are one interval [elo, ehi), stored per row; a row with none ([C, 0)) is masked everywhere
+  // and sits at the mask level, where every key counts (uniform P).  Step flags (wave 0 holds
+  // the BQ rows): 1 = no row sees this key block and none is empty (P = dS = 0 exactly: the
+  // step is skipped), 2 = every row sees the whole block (no per-element mask).
+  auto ld_store = [&](int buf, int tq) {
     if (tid < BQ) {
       const float lv = p.l_f16 ? f16_to_f32((uint16_t)lraw) : __builtin_bit_cast(float, lraw);
       const float dv = p.d_bf16 ? bf16_to_f32((uint16_t)draw) : __builtin_bit_cast(float, draw);
       lb0[buf * BQ + tid] = ldv ? lv : __builtin_inff();
       db0[buf * BQ + tid] = ldv ? dv : 0.f;
+      if constexpr (MSK) {
+        const int q = tq + tid;
+        int64_t lo = 0, hi = p.C;
+        if (p.mask.ranges) {
+          lo = rraw.x;
+          hi = min((int64_t)rraw.y, (int64_t)p.C);
+        }
+        if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
+        if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
+        const bool empty = lo >= hi;
+        const int elo = empty ? p.C : (int)lo, ehi = empty ? 0 : (int)hi;
+        rg0[buf * BQ + tid] = make_int2(elo, ehi);
+        const bool skip = !ldv || (!empty && (ehi <= k0 || elo >= k0 + BK));
+        const bool full = !ldv || (!empty && elo <= k0 && ehi >= min(k0 + BK, p.C));
+        const uint64_t act = __ballot(true);
+        const int f = (__ballot(skip) == act ? 1 : 0) | (__ballot(full) == act ? 2 : 0);
+        if (tid == 0) fl0[buf] = f;
+      }
+    }
+  };
+
+  // MSK: LDS-DMA of a step's additive-mask tile — query rows t..t+BQ of head h, this block's
+  // BK keys — row-major into dst (2 rows per 1-KiB piece, lane l at byte 16l: row 2n + l/32,
+  // keys k0 + 4(l%32)..+3); rows past R read as zeros.  No staging registers (at D = 256 the
+  // kernel is at the register limit).  Needs C % 4 == 0 (16-byte rows; see bwd_fast_eligible).
+  auto am_issue = [&](int h, int t, float* dst) {
+    if (!p.mask.amask) return;
+    constexpr int PPW = BQ / 2 / (NT / 64);
+    const char* head = (const char*)(p.mask.amask + (int64_t)(b * p.H + h) * p.R * p.C);
+    const int ln = __lane_id();  // recomputed here rather than held across the step
+    const int voff = (ln >> 5) * p.C * 4 + k0 * 4 + 16 * (ln & 31);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);  // piece indices in scalar registers
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int n = wv + (NT / 64) * i, row = t + 2 * n;
+      const int64_t left = (int64_t)(p.R - row) * p.C * 4;
+      lds_dma16(head + (int64_t)row * p.C * 4, left <= 0 ? 0 : (int)min(left, (int64_t)0x7fffffff),
+                voff, (char*)dst + n * 1024);
     }
   };
 
@@ -442,13 +581,21 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   for (int dt = 0; dt < ND; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
   const float c = p.c_log2, sc = p.scale;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+  // P = exp2(S·c − L); MSK: rows at the mask level take the rounded product first.
+  auto pexp = [&](float x, float l) {
+    if constexpr (MSK)
+      return __builtin_amdgcn_exp2f(l < kMaskLevel ? mul_rn(x, c) - l : __builtin_fmaf(x, c, -l));
+    else
+      return __builtin_amdgcn_exp2f(__builtin_fmaf(x, c, -l));
+  };
 
   if (nsteps > 0) {
     qd.issue(qhead(kvh), qbeg, qb0);
     od.issue(ohead(kvh), qbeg, ob0);
+    if (MSK) am_issue(kvh, qbeg, am0);
     ld_load(kvh, qbeg);
     wait_vm();
-    ld_store(0);
+    ld_store(0, qbeg);
   }
   // Unconditionally drained before the loop: otherwise the K/V fragment loads count as
   // possibly pending at the loop header and hipcc puts a vmcnt(0) before their first use in
@@ -467,10 +614,17 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     const int tn = t < qlast ? t + BQ : qbeg;
     const int hn = t < qlast ? h : h + p.Hkv;
     if (has_next) ld_load(hn, tn);
-    if (!spread_dma<DP>() && has_next) {
-      qd.issue(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB);
-      od.issue(ohead(hn), tn, ob0 + (cur ^ 1) * TILEB);
-    }
+    // MSK at D = 256 spills a few registers; their reloads wait for every outstanding load
+    // (vmcnt(0)), so the next step's tiles are issued after the S/dP chains, where none is left.
+    constexpr bool late_dma = MSK && DP >= 256;
+    auto issue_next = [&]() {
+      if (MSK && has_next) am_issue(hn, tn, am0 + (cur ^ 1) * BQ * BK);
+      if (!spread_dma<DP>() && has_next) {
+        qd.issue(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB);
+        od.issue(ohead(hn), tn, ob0 + (cur ^ 1) * TILEB);
+      }
+    };
+    if (!late_dma) issue_next();
     BST(0);
     // The next step's Q and dO tiles: one LDS-DMA piece after every other MFMA of the first
     // chain, so each piece's issue cost sits in an MFMA gap.
@@ -489,6 +643,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     const char* ot = ob0 + cur * TILEB;
     const float* lt = lb0 + cur * BQ;
     const float* dtl = db0 + cur * BQ;
+    const int2* rgt = rg0 + cur * BQ;
+    const float* amt = am0 + cur * BQ * BK;  // + this lane's key column (at the reads)
+    const int flags = MSK ? __builtin_amdgcn_readfirstlane(fl0[cur]) : 0;
 
     f32x16 s[NJ], dp[NJ];
 #pragma unroll
@@ -503,7 +660,55 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
           v[j][4 * g4] = x.x; v[j][4 * g4 + 1] = x.y; v[j][4 * g4 + 2] = x.z; v[j][4 * g4 + 3] = x.w;
         }
     };
+    // MSK: bit 16j + i of mbits = accumulator element (j, i) outside its row's interval
+    // (query t + 32j + 8(i>>2) + 4hh + (i&3), this lane's key), computed before the S chain
+    // from two 16-byte LDS reads per four rows — one wait per step, not one per element.
+    uint32_t mbits = 0u;
+    auto mask_bits = [&]() {
+      const int hl = (DP >= 256 ? __lane_id() : lane) >> 5;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int ql0 = 32 * j + 8 * g4 + 4 * hl;
+          const int4 ra = *reinterpret_cast<const int4*>(rgt + ql0);
+          const int4 rb = *reinterpret_cast<const int4*>(rgt + ql0 + 2);
+          const int lo[4] = {ra.x, ra.z, rb.x, rb.z}, hi[4] = {ra.y, ra.w, rb.y, rb.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            mbits |= (ki < lo[e] || ki >= hi[e] ? 1u : 0u) << (16 * j + 4 * g4 + e);
+        }
+    };
+    // At D <= 128 before the S chain (its latency hides there); at D = 256 (register limit)
+    // after it, where the chain's fragment registers are free.
+    if (DP <= 128 && MSK && !(flags & 2)) mask_bits();
     auto apply_mask = [&]() {
+      if constexpr (MSK) {
+        if (DP > 128 && !(flags & 2)) mask_bits();
+        if (!p.mask.amask && (flags & 2)) return;
+        // Additive-mask values of the tile (LDS, lanes read consecutive keys), all issued
+        // before the first use; at D = 256 (register limit) eight at a time.
+        constexpr int G = DP >= 256 ? 4 : 16;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i0 = 0; i0 < 16; i0 += G) {
+            float a[G];
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+              const int ii = i0 + i;
+              // At D = 256 the lane's offsets are recomputed rather than held across the step.
+              const int ln = DP >= 256 ? __lane_id() : lane;
+              const int col = (DP >= 256 ? __builtin_amdgcn_readfirstlane(wave) : wave) * 32 + (ln & 31);
+              a[i] = p.mask.amask ? amt[(32 * j + 8 * (ii >> 2) + 4 * (ln >> 5) + (ii & 3)) * BK + col] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < G; ++i)
+              s[j][i0 + i] = ((mbits >> (16 * j + i0 + i)) & 1u) ? kMaskValue : s[j][i0 + i] + a[i];
+            if (G < 16) __builtin_amdgcn_sched_barrier(0);
+          }
+        return;
+      }
       if ((p.mask.causal && k0 + BK - 1 > t) || p.mask.window) {
         MFA_KEEP_BRANCH();
         {
@@ -515,7 +720,12 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
         }
       }
     };
-    if constexpr (DP <= 128) {
+    if (MSK && (flags & 1)) {
+      // No row of this step sees the key block: nothing to add (the next tiles' DMA still
+      // lands before the barrier).
+      if (late_dma) issue_next();
+      static_assert(!MSK || !spread_dma<DP>(), "mask steps issue the next tiles up front");
+    } else if constexpr (DP <= 128) {
       // S = Q·K^T; masks; dP = dO·V^T with P = exp2(S·c − L) computed between its MFMAs;
       // dV^T += dO^T·P with dS = P∘(dP·scale − D) computed between its MFMAs; dK^T += Q^T·dS.
       // The S and dP accumulators are read once each into VGPR values (P, and dS eight at a
@@ -539,7 +749,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
 #pragma unroll
           for (int e = 0; e < EPM; ++e) {
             const int idx = i * EPM + e, jj = idx >> 4, ii = idx & 15;
-            pf[jj][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[jj][ii], c, -lv[jj][ii]));
+            pf[jj][ii] = pexp(s[jj][ii], lv[jj][ii]);
           }
         });
       }
@@ -578,6 +788,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       // S and dP chains together (the registers do not hold a hook's working set beside
       // both chains), then P, then dS threaded through the dV chain.
       dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase, dma_hook);
+      if (late_dma) issue_next();
       apply_mask();
       BST(1);
       static_assert(NJ == 1, "D = 256 runs 32-query steps");
@@ -589,7 +800,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       for (int g4 = 0; g4 < 4; ++g4) ldg(lt, g4, lq[g4]);
 #pragma unroll
       for (int ii = 0; ii < 8; ++ii)
-        s[0][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[0][ii], c, -lq[ii >> 2][ii & 3]));
+        s[0][ii] = pexp(s[0][ii], lq[ii >> 2][ii & 3]);
       pb[0] = A::pack(s[0], 0);
       BST(2);
       {
@@ -600,7 +811,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
         tr_chain<A, NJ, ND>(ot, trb, pb, dv, [&](int i) {
           if (i < 8) {
             const int ii = 8 + i;
-            s[0][ii] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[0][ii], c, -lq[ii >> 2][ii & 3]));
+            s[0][ii] = pexp(s[0][ii], lq[ii >> 2][ii & 3]);
             if (i == 7) pb[1] = A::pack(s[0], 1);
           }
           const int ii = i, grp = ii >> 2, k = ii & 3;
@@ -616,6 +827,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       // D = 256 (previous schedule) runs at the register limit: S and dP chains together, then the softmax, then
       // dV and dK together.
       dual_rows_chain<A, NJ>(qt, ot, kf, vf, s, dp, rbase, dma_hook);
+      if (late_dma) issue_next();
       apply_mask();
       float lv[NJ][16], dv_[NJ][16];
       lds4(lt, lv);
@@ -624,7 +836,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][i], c, -lv[j][i]));
+          const float pv = pexp(s[j][i], lv[j][i]);
           s[j][i] = pv;
           dp[j][i] = pv * __builtin_fmaf(dp[j][i], sc, -dv_[j][i]);
         }
@@ -660,7 +872,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     }
     wait_vm();
     BST(5);
-    if (has_next) ld_store(cur ^ 1);
+    if (has_next) ld_store(cur ^ 1, tn);
     __syncthreads();
     BST(6);
     cur ^= 1;
@@ -699,10 +911,12 @@ template <class E, int DP>
 static hipError_t launch_bwd_q_fast(const BwdParams& p, hipStream_t stream) {
   constexpr int BT = BwdFastCfg<DP>::BT;
   constexpr int LDS = 4 * BT * DP * 2;
-  auto kern = mfa_bwd_q_fast_kernel<E, DP, BT>;
   BwdParams q = p;
   q.nblk = (p.R + 127) / 128;
-  return launch(kern, dim3(q.nblk * p.B * p.H), dim3(256), LDS, stream, q);
+  const dim3 grid(q.nblk * p.B * p.H);
+  if (p.mask.amask || p.mask.ranges)
+    return launch(mfa_bwd_q_fast_kernel<E, DP, BT, true>, grid, dim3(256), LDS + 128, stream, q);
+  return launch(mfa_bwd_q_fast_kernel<E, DP, BT>, grid, dim3(256), LDS, stream, q);
 }
 
 template <class E, int DP>
@@ -712,6 +926,11 @@ static hipError_t launch_bwd_kv_fast(const BwdParams& p, hipStream_t stream) {
   BwdParams q = p;
   q.nblk = (p.C + 127) / 128;
   const dim3 grid(q.nblk * p.B * p.Hkv);
+  if (p.mask.amask || p.mask.ranges) {
+    if (p.k.prec != P_FP16 && p.k.prec != P_BF16) return hipErrorNotSupported;
+    return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ, SRC_SAME, true>, grid, dim3(256),
+                  LDS + 2 * BQ * 8 + 2 * BQ * 128 * 4 + 16, stream, q);
+  }
   if (p.k.prec == P_INT8) return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ, SRC_I8>, grid, dim3(256), LDS, stream, q);
   if (p.k.prec == P_INT4) return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ, SRC_I4>, grid, dim3(256), LDS, stream, q);
   return launch(mfa_bwd_kv_fast_kernel<E, DP, BQ>, grid, dim3(256), LDS, stream, q);
@@ -742,7 +961,9 @@ namespace mfa {
   template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT>(BwdParams);   \
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ>(BwdParams);    \
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I8>(BwdParams); \
-  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I4>(BwdParams);
+  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I4>(BwdParams); \
+  template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, true>(BwdParams);   \
+  template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_SAME, true>(BwdParams);
 MFA_BF_INST(F16, 64)
 MFA_BF_INST(F16, 128)
 MFA_BF_INST(F16, 256)

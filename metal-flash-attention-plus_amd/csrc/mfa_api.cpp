@@ -1077,8 +1077,13 @@ bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int 
     }
     if (op->prec != prec || !op->vec || op->sd != 1 || op->bscale) return false;
   }
-  if (p.mask.amask || p.mask.ranges) return false;
-  if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok) return false;
+  // Additive masks and ranges run the kernels' element-wise mask instantiation (16-bit K/V),
+  // which also covers fully masked rows, so it needs no skip_ok.
+  const bool msk = p.mask.amask || p.mask.ranges;
+  if (msk && ksrc != 0) return false;
+  // The backwardKeyValue mask tile moves by 16-byte LDS-DMA: 16-byte aligned rows.
+  if (p.mask.amask && (p.C % 4 != 0 || ((uintptr_t)p.mask.amask & 15) != 0)) return false;
+  if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok && !msk) return false;
   // Dense O, dQ, dK, dV rows.
   if (p.o_sd != 1 || p.dq_sd != 1 || p.dk_sd != 1 || p.dv_sd != 1) return false;
   // Tiles are addressed per head with 32-bit buffer offsets.
@@ -1119,9 +1124,15 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
       // Quantised K/V with 16-bit Q reach here only for backwardKeyValue alone (see
       // quantized_backward): its fast kernel widens them in registers.
       const bool fast_kv = fast || (!big && ksrc > 0 && bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true));
-      hipError_t e = big       ? mfa::bwd_bigd_dispatch(p, 1, elem, stream)
-                     : fast_kv ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream)
-                               : hipErrorNotSupported;
+      // D = 256 calls the tuned kernel does not take (strides, transposes): the generic kernel.
+      // MFA_BWD256_BIGD=1 runs the D-blocked kernel in two 128-column slices instead (measured
+      // 3x slower: each slice recomputes S and dP over all 256 columns on 32-row tiles).
+      const char* b256 = getenv("MFA_BWD256_BIGD");
+      const bool blocked = !big && !fast_kv && DP == 256 && elem != 0 && ksrc == 0 && qsrc == 0 &&
+                           b256 && b256[0] == '1';
+      hipError_t e = big || blocked ? mfa::bwd_bigd_dispatch(p, 1, elem, stream)
+                     : fast_kv      ? mfa::bwd_fast_dispatch(p, 1, elem, DP, stream)
+                                    : hipErrorNotSupported;
       if (big && e == hipErrorNotSupported)
         return fail(MFA_ERR_UNSUPPORTED, "head dimension %d: mixed operand precisions", p.D);
       if (e == hipErrorNotSupported) e = mfa::bwd_kv_dispatch(p, elem, DP, ksrc, qsrc, stream);

@@ -181,3 +181,97 @@ def test_fwd_bwd_c5_slice(gpu, D):
     B, H, S = 1, 2, 1024
     Q, K, V, dO = (gaussian((B, H, S, D), 60 + i) * 0.5 for i in range(4))
     check_backward(Q, K, V, dO, FP16, 5e-2, 1e-1)
+
+
+# ------------------------------------------------ additive masks and ranges on the tuned kernels
+# Additive masks and sparse ranges run the tuned backward kernels' mask instantiation
+# (attention_bwd_fast.hip, MSK = true): every mask element by element, fully masked rows on the
+# exact-product path, the mask tile staged by LDS-DMA.  Before, these calls ran the generic
+# kernels (at D = 256 one whose dK/dV accumulators spill ~470 registers).
+def masked_case(kind, B, H, Hkv, R, C, seed):
+    kw = {}
+    if kind in ("amask", "amask_causal"):
+        kw["amask"] = gaussian((B, H, R, C), seed) * 2
+        kw["causal"] = kind == "amask_causal"
+    elif kind == "window_amask":
+        kw["amask"] = gaussian((B, H, R, C), seed) * 2
+        kw["window"] = 40
+    else:
+        rng = np.random.default_rng(seed)
+        lo = rng.integers(0, C, size=(B, Hkv, R)).astype(np.uint32)
+        if kind == "ranges_causal":  # key lo <= row stays: no row masked everywhere (FP16 L)
+            lo = np.minimum(lo, np.arange(R, dtype=np.uint32))
+        hi = np.minimum(lo + rng.integers(1, 120, size=lo.shape), C).astype(np.uint32)
+        lo[..., 7::13] = 0  # some rows see every key
+        hi[..., 7::13] = C
+        kw["ranges"] = np.ascontiguousarray(np.stack([lo, hi], -1))
+        kw["causal"] = kind == "ranges_causal"
+    return kw
+
+
+@pytest.mark.parametrize("prec", [FP16, BF16])
+@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("kind", ["amask", "ranges", "amask_causal", "ranges_causal",
+                                  "window_amask"])
+def test_masked_backward_tuned_kernels(gpu, prec, D, kind):
+    B, H, Hkv, R, C = 1, 4, 2, 200, 260
+    Q, dO = gaussian((B, H, R, D), 70) * 0.5, gaussian((B, H, R, D), 71) * 0.5
+    K, V = gaussian((B, Hkv, C, D), 72) * 0.5, gaussian((B, Hkv, C, D), 73) * 0.5
+    kw = masked_case(kind, B, H, Hkv, R, C, 74 + D)
+    mfa.last_launches()
+    check_backward(Q, K, V, dO, prec, 5e-2, 1e-1, **kw)
+    names = [x["name"] for x in mfa.last_launches()]
+    assert any(n.startswith("mfa_bwd_q_fast_kernel") and n.endswith("true>") for n in names), names
+    assert any(n.startswith("mfa_bwd_kv_fast_kernel") and n.endswith("true>") for n in names), names
+
+
+def test_masked_backward_fully_masked_rows_match_generic(gpu, monkeypatch):
+    # Rows whose every key is masked keep L at the mask level (FP32 L).  The backward then
+    # recomputes P = exp2(S·c − L) with the product rounded first (the generic kernel's and the
+    # reference's formula, which loses L's log2(C) at that magnitude, so the oracle's exact
+    # softmax is not the target here): the tuned kernels' mask instantiation must give the
+    # generic kernels' gradients on such rows, and the oracle's on every other row.
+    B, H, R, C, D = 1, 2, 130, 190, 128
+    Q, dO = gaussian((B, H, R, D), 80) * 0.5, gaussian((B, H, R, D), 81) * 0.5
+    K, V = gaussian((B, H, C, D), 82) * 0.5, gaussian((B, H, C, D), 83) * 0.5
+    lo = (np.arange(R) % C).astype(np.uint32)
+    hi = np.minimum(lo + 50, C).astype(np.uint32)
+    hi[5::9] = lo[5::9]
+    empty = hi <= lo
+    ranges = np.ascontiguousarray(np.broadcast_to(np.stack([lo, hi], -1), (B, H, R, 2)))
+    base = mfa.AttentionDescriptor.make(low_precision=True, precision=FP16,
+                                        low_precision_intermediates=False,
+                                        sparse_mask=mfa.MaskType.sparseRanges)
+    desc = mfa.MultiHeadDescriptor.make(base, B, H, R, D, C=C)
+    dev = "cuda:0"
+    q, k, v, do = (to_device(x, FP16) for x in (Q, K, V, dO))
+    mask = torch.from_numpy(ranges.view(np.int32)).to(dev)
+
+    def grads():
+        o = torch.empty((B, H, R, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, R), dtype=torch.float32, device=dev)
+        dbuf = torch.empty((B, H, R), dtype=torch.float32, device=dev)
+        dq, dk, dv = (torch.full((B, H, n, D), float("nan"), dtype=torch.float32, device=dev)
+                      for n in (R, C, C))
+        mha = mfa.MultiHeadAttention()
+        mha.forward(desc, q, k, v, o, l, mask=mask)
+        mfa.last_launches()
+        mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf, mask=mask)
+        torch.cuda.synchronize()
+        return ({"dQ": dq.cpu().numpy(), "dK": dk.cpu().numpy(), "dV": dv.cpu().numpy()},
+                [x["name"] for x in mfa.last_launches()])
+
+    fast, names = grads()
+    assert any(n.startswith("mfa_bwd_kv_fast_kernel") and n.endswith("true>") for n in names), names
+    monkeypatch.setenv("MFA_DISABLE_FAST", "1")
+    gen, names_g = grads()
+    assert not any("fast" in n for n in names_g), names_g
+    for name in ("dQ", "dK", "dV"):
+        assert np.isfinite(fast[name]).all(), name
+        scale = max(1.0, float(np.abs(gen[name]).max()))
+        e = maxerr(fast[name], gen[name]) / scale
+        assert e <= 1e-3, f"{name} differs from the generic kernel by {e}"
+    ref = ol.attention(seen(Q, FP16), seen(K, FP16), seen(V, FP16), dO=seen(dO, FP16),
+                       ranges=ranges)
+    e = maxerr(fast["dQ"][:, :, ~empty], ref["dQ"][:, :, ~empty])
+    assert e <= 5e-2, f"dQ max error {e} on rows with keys"

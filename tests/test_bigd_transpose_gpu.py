@@ -129,7 +129,7 @@ def test_transposes_fwd_bwd_fp32(gpu, tr):
 @pytest.mark.parametrize("tr", [(True, True, True, True), (False, False, False, True),
                                 (True, False, True, False)],
                          ids=lambda t: "".join("T" if x else "N" for x in t))
-@pytest.mark.parametrize("prec,D", [(FP16, 128), (BF16, 64), (FP16, 320)])
+@pytest.mark.parametrize("prec,D", [(FP16, 128), (BF16, 64), (FP16, 256), (FP16, 320)])
 def test_transposes_fwd_bwd_mixed(gpu, tr, prec, D):
     B, H, S = 1, 2, 200
     Q, K, V, dO = (gaussian((B, H, S, D), 730 + i, 0.5) for i in range(4))

@@ -61,8 +61,8 @@ def test_c5_forward_and_backward_phases():
     assert f["name"] == "mfa_fwd2_share_kernel<F16, 256, 32, false, false, false, false>"
     q = one(mfa.multihead_plan(d, K.backwardQuery))
     kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
-    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32>"
-    assert kv["name"] == "mfa_bwd_kv_fast_kernel<F16, 256, 32, 0>"
+    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32, false>"
+    assert kv["name"] == "mfa_bwd_kv_fast_kernel<F16, 256, 32, 0, false>"
     assert q["workgroups"] == 32 * 8 * 32 and kv["workgroups"] == 32 * 8 * 32
     for r in (f, q, kv):
         assert r["lds_bytes"] <= 160 * 1024
@@ -104,11 +104,11 @@ def test_quantized_plans():
     # backwardQuery: one dequantisation pass per quantised operand (kv_dequant.hip), then the
     # tuned 16-bit kernel on the dense copies (K/V tiles stream through LDS).
     assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardQuery)][2] == \
-        "mfa_bwd_q_fast_kernel<F16, 128, 64>"
+        "mfa_bwd_q_fast_kernel<F16, 128, 64, false>"
     # backwardKeyValue reads each key block's K/V once into registers and widens them there:
     # the INT8 instantiation (SRC_I8 = 1), no pass.
     assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardKeyValue)] == \
-        ["mfa_bwd_kv_fast_kernel<F16, 128, 64, 1>"]
+        ["mfa_bwd_kv_fast_kernel<F16, 128, 64, 1, false>"]
     # INT4 K/V with an FP16 Q: the same on-load kernel (SRC_I4 = 2).
     q4h = mfa.quantized_descriptor(base, P.FP16, P.INT4, P.INT4, B=1, H=16)
     assert [r["name"] for r in mfa.quantized_plan(q4h)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2, 1, 3, 12, 14>"]

@@ -2,7 +2,8 @@
 
 Usage: python tools/ab_env.py WORKLOAD VAR=a,b,c [VAR2=x,y] — times each setting by HIP
 events (median of 5 rounds of 20 launches), interleaving settings round by round.
-WORKLOAD: c3_int8_exact | c3_fp16 | c2 | sparse (the bench's block-sparse row).  A value "-"
+WORKLOAD: c3_int8_exact | c3_fp16 | c2 | sparse (the bench's block-sparse row) |
+bwd256[_amask] | bwd128[_amask] (backwardKeyValue with or without an additive mask).  A value "-"
 unsets the variable (the library default).
 """
 import itertools
@@ -71,6 +72,31 @@ def workload(name, dev="cuda:0"):
         pairs = int((rows[0, 0, :, 1].astype(np.int64) - rows[0, 0, :, 0]).sum()) * B * H
         return (lambda: mfa.MultiHeadAttention().forward(desc, q, k, v, o, l, mask=mask,
                                                          stream=stream)), 4.0 * D * pairs
+    if name.startswith("bwd256") or name.startswith("bwd128"):
+        # backwardKeyValue at D = 256 / 128 with an additive mask (bwd*_amask) or none: 4 GEMMs
+        # per tile.
+        B, H, S, D = 1, 16, 2048, int(name[3:6])
+        q, k, v, do = (u((B, H, S, D), torch.float16) for _ in range(4))
+        mask = u((B, H, S, S), torch.float32) if name.endswith("_amask") else None
+        if name.endswith("_ranges"):  # every key in range: the mask path with no amask traffic
+            import numpy as np
+            rows = np.zeros((B, H, S, 2), dtype=np.uint32)
+            rows[..., 1] = S
+            mask = torch.from_numpy(rows.view(np.int32)).to(dev)
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+        dbuf = torch.empty((B, H, S), dtype=torch.bfloat16, device=dev)
+        dq, dk, dv = (torch.empty((B, H, S, D), dtype=torch.float32, device=dev) for _ in range(3))
+        base = mfa.AttentionDescriptor.make(
+            low_precision=True, precision=mfa.Precision.FP16,
+            sparse_mask=mfa.MaskType.sparseRanges if name.endswith("_ranges") else None)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+        mha = mfa.MultiHeadAttention()
+        mha.forward(desc, q, k, v, o, l, mask=mask, stream=stream)
+        mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf, mask=mask, phase="query",
+                     stream=stream)
+        return (lambda: mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf, mask=mask,
+                                     phase="keyValue", stream=stream)), 8.0 * B * H * S * S * D
     raise SystemExit(f"unknown workload {name}")
 
 
