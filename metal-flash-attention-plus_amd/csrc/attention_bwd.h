@@ -227,14 +227,18 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_q_kernel(BwdParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
-// backwardKeyValue: grid = nblk x B x H_kv; NW waves x 32 keys; traverses every query head of
-// the group and every query tile.
-template <class A, int DP, int BT, int NW, int QSRC>
+// backwardKeyValue: grid = (nblk x B x H_kv, DP / DC); NW waves x 32 keys; traverses every
+// query head of the group and every query tile.  Workgroup y accumulates dK/dV columns
+// [DC·y, DC·y + DC) only: at DP = 256 (DC = 128) the 256-column accumulators beside the
+// fragments and staging registers spilled ~470 registers; the two column halves each recompute
+// S and dP instead (1.5x the MFMA work of the unsplit kernel, no scratch).
+template <class A, int DP, int BT, int NW, int QSRC, int DC = DP>
 __global__ void __launch_bounds__(NW * 64) mfa_bwd_kv_kernel(BwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = NW * 64;
   constexpr int BK = NW * 32;
   constexpr int NJ = BT / 32;
+  constexpr int NDC = DC / 32;
   constexpr int TILEB = A::is_f32 ? BT * (DP + 1) * 4 : BT * DP * 2;
   char* const qb0 = smem;
   char* const ob0 = smem + 2 * TILEB;
@@ -269,9 +273,10 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_kv_kernel(BwdParams p) {
   const int ngroup = (p.H - kvh + p.Hkv - 1) / p.Hkv;
   const int nsteps = ntile * ngroup;
 
-  f32x16 dk[DP / 32], dv[DP / 32];
+  const int oc0 = (int)blockIdx.y * DC;
+  f32x16 dk[NDC], dv[NDC];
 #pragma unroll
-  for (int dt = 0; dt < DP / 32; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+  for (int dt = 0; dt < NDC; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
   const float c = p.c_log2;
 
   Stager<A, BT, DP, NT, QSRC> sq;
@@ -353,9 +358,9 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_kv_kernel(BwdParams p) {
         const typename A::frag pb = A::pack(s[j], ks);
         const typename A::frag sb = A::pack(dp[j], ks);
 #pragma unroll
-        for (int d = 0; d < DP / 32; ++d) {
-          dv[d] = A::mma(A::read_tr(ot, j * 32, ks, d * 32, lane), pb, dv[d]);
-          dk[d] = A::mma(A::read_tr(qt, j * 32, ks, d * 32, lane), sb, dk[d]);
+        for (int d = 0; d < NDC; ++d) {
+          dv[d] = A::mma(A::read_tr(ot, j * 32, ks, oc0 + d * 32, lane), pb, dv[d]);
+          dk[d] = A::mma(A::read_tr(qt, j * 32, ks, oc0 + d * 32, lane), sb, dk[d]);
         }
       }
     }
@@ -369,10 +374,10 @@ __global__ void __launch_bounds__(NW * 64) mfa_bwd_kv_kernel(BwdParams p) {
     float* ok = p.dk + slice + (int64_t)ki * p.dk_ss;
     float* ov = p.dv + slice + (int64_t)ki * p.dv_ss;
 #pragma unroll
-    for (int d = 0; d < DP / 32; ++d) {
+    for (int d = 0; d < NDC; ++d) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int dd = d * 32 + 8 * g + 4 * hh;
+        const int dd = oc0 + d * 32 + 8 * g + 4 * hh;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (dd + e < p.D) {
@@ -396,8 +401,15 @@ template <class A, int DP, int BT, int NW, int QSRC>
 hipError_t launch_bwd_kv(const BwdParams& p, hipStream_t stream) {
   constexpr int TILEB = A::is_f32 ? BT * (DP + 1) * 4 : BT * DP * 2;
   constexpr int LDS = 4 * TILEB + 4 * BT * 4;
-  auto kern = mfa_bwd_kv_kernel<A, DP, BT, NW, QSRC>;
-  return launch(kern, dim3(p.nblk * p.B * p.Hkv), dim3(NW * 64), LDS, stream, p);
+  constexpr int DC = DP >= 256 ? (A::is_f32 ? 64 : 128) : DP;  // dK/dV columns per workgroup
+  if constexpr (DC != DP) {
+    const char* e = getenv("MFA_BWD256_SPLIT");  // development A/B: 0 = unsplit kernel
+    if (e && e[0] == '0')
+      return launch(mfa_bwd_kv_kernel<A, DP, BT, NW, QSRC>, dim3(p.nblk * p.B * p.Hkv),
+                    dim3(NW * 64), LDS, stream, p);
+  }
+  auto kern = mfa_bwd_kv_kernel<A, DP, BT, NW, QSRC, DC>;
+  return launch(kern, dim3(p.nblk * p.B * p.Hkv, DP / DC), dim3(NW * 64), LDS, stream, p);
 }
 
 }  // namespace mfa

@@ -78,3 +78,13 @@ def test_hot_kernels_fit_register_file(kernels):
     for n, k in kernels.items():
         if any(f in n for f in HOT):
             assert k["vgpr"] <= 512, (n, k)
+
+
+def test_generic_backward_kv_d256_does_not_spill(kernels):
+    # The generic backwardKeyValue kernel (strided / transposed D = 256 16-bit calls) splits its
+    # dK/dV columns over two workgroups (attention_bwd.h, DC = 128): no register spills (it spilled
+    # ~470 before).  Its small fixed stack (no spill count) is the Stager's indexed staging.
+    gen = {n: k for n, k in kernels.items()
+           if "mfa_bwd_kv_kernel" in n and "Arith16" in n and "ELi256E" in n}
+    assert gen, "generic D = 256 backwardKeyValue kernels not found"
+    assert all(k["vgpr_spill"] == 0 for k in gen.values()), gen
