@@ -166,46 +166,8 @@ __device__ __forceinline__ void tr_chain(const char* tile, const int (&trb)[2], 
 }
 
 // ---------------------------------------------------------------------------------------
-// Register-staged twin of DmaA for per-tensor quantised K/V tiles (backwardQuery): each thread
-// loads the same (piece, lane) chunks the LDS-DMA would, widens them to the exact integers
-// q - zp (the scales stay folded, as in the dequantisation pass) and writes them to the same
-// TileA image bytes — no pass, no dense 16-bit copy.
-template <class E, int DP, int ROWS, int NT, int SRC>
-struct QStageA {
-  static constexpr int NW = NT / 64, PPRB = DP / 64, NPIECE = ROWS * DP * 2 / 1024;
-  static constexpr int PPW = NPIECE / NW;
-  uint4 raw[PPW];
-  __device__ __forceinline__ void load(const Operand& op, int b, int hx, int t, int nrows, int D) {
-    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int n = w + NW * i, rblk = n / PPRB, sub = 2 * (n % PPRB) + (l >> 5);
-      const int r7 = (l & 31) >> 2, ch = 4 * sub + ((l & 3) ^ ((2 * rblk + (r7 >> 2)) & 3));
-      const int row = t + rblk * 8 + r7, d0 = ch * 8;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (row < nrows && d0 < D)
-        v = load_qchunk<SRC>(op, (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)row * op.ss, d0, D);
-      raw[i] = v;
-    }
-  }
-  __device__ __forceinline__ void store(char* dst, const Operand& op, int t, int nrows, int D) const {
-    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const float zp = (float)op.zp;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int n = w + NW * i, rblk = n / PPRB, sub = 2 * (n % PPRB) + (l >> 5);
-      const int r7 = (l & 31) >> 2, ch = 4 * sub + ((l & 3) ^ ((2 * rblk + (r7 >> 2)) & 3));
-      const bool valid = t + rblk * 8 + r7 < nrows && ch * 8 < D;
-      const uint4 v = valid ? dequant_fast<E, SRC>(raw[i], zp) : make_uint4(0u, 0u, 0u, 0u);
-      *reinterpret_cast<uint4*>(dst + n * 1024 + 16 * l) = v;
-    }
-  }
-};
-
 // backwardQuery.  Grid: nblk x B x H, heaviest causal blocks first.  BT keys per tile.
-// KVQ: K/V storage — SRC_SAME (16-bit, LDS-DMA) or SRC_I8 / SRC_I4 per-tensor quantised
-// (QStageA: widened on the way to LDS).
-template <class E, int DP, int BT, bool MSK = false, int KVQ = SRC_SAME>
+template <class E, int DP, int BT, bool MSK = false>
 __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   using A = Arith16<E, DP>;
   constexpr int NT = 256, BQ = 128, NJ = BT / 32, DS = DP / 16, ND = DP / 32;
@@ -301,15 +263,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   vd.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
   const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
   const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
-  QStageA<E, DP, BT, NT, KVQ == SRC_SAME ? SRC_I8 : KVQ> kq, vq;
   if (kbeg < kend) {
-    if constexpr (KVQ != SRC_SAME) {
-      kq.load(p.k, b, kvh, kbeg, p.C, p.D);
-      vq.load(p.v, b, kvh, kbeg, p.C, p.D);
-    } else {
-      kd.issue(khead, kbeg, kb0);
-      vd.issue(vhead, kbeg, vb0);
-    }
+    kd.issue(khead, kbeg, kb0);
+    vd.issue(vhead, kbeg, vb0);
   }
 
   // D = scale · Σ_d dO∘O (computeD, Softmax.swift:31-236): dO as stored (16-bit), O fp32.
@@ -355,23 +311,12 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   for (int dt = 0; dt < ND; ++dt) dq[dt] = zero16();
 
   wait_vm();
-  if constexpr (KVQ != SRC_SAME) {
-    if (kbeg < kend) {
-      kq.store(kb0, p.k, kbeg, p.C, p.D);
-      vq.store(vb0, p.v, kbeg, p.C, p.D);
-    }
-  }
   __syncthreads();
   int cur = 0;
   for (int t = kbeg; t < kend; t += BT) {
     if (t + BT < kend) {
-      if constexpr (KVQ != SRC_SAME) {
-        kq.load(p.k, b, kvh, t + BT, p.C, p.D);
-        vq.load(p.v, b, kvh, t + BT, p.C, p.D);
-      } else {
-        kd.issue(khead, t + BT, kb0 + (cur ^ 1) * TILEB);
-        vd.issue(vhead, t + BT, vb0 + (cur ^ 1) * TILEB);
-      }
+      kd.issue(khead, t + BT, kb0 + (cur ^ 1) * TILEB);
+      vd.issue(vhead, t + BT, vb0 + (cur ^ 1) * TILEB);
     }
     const char* kt = kb0 + cur * TILEB;
     const char* vt = vb0 + cur * TILEB;
@@ -457,12 +402,6 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
       });
     }
     wait_vm();
-    if constexpr (KVQ != SRC_SAME) {
-      if (t + BT < kend) {
-        kq.store(kb0 + (cur ^ 1) * TILEB, p.k, t + BT, p.C, p.D);
-        vq.store(vb0 + (cur ^ 1) * TILEB, p.v, t + BT, p.C, p.D);
-      }
-    }
     __syncthreads();
     cur ^= 1;
   }
@@ -975,12 +914,6 @@ static hipError_t launch_bwd_q_fast(const BwdParams& p, hipStream_t stream) {
   BwdParams q = p;
   q.nblk = (p.R + 127) / 128;
   const dim3 grid(q.nblk * p.B * p.H);
-  if (p.k.prec == P_INT8 || p.k.prec == P_INT4) {
-    if (p.mask.amask || p.mask.ranges) return hipErrorNotSupported;
-    return p.k.prec == P_INT8
-               ? launch(mfa_bwd_q_fast_kernel<E, DP, BT, false, SRC_I8>, grid, dim3(256), LDS, stream, q)
-               : launch(mfa_bwd_q_fast_kernel<E, DP, BT, false, SRC_I4>, grid, dim3(256), LDS, stream, q);
-  }
   if (p.mask.amask || p.mask.ranges)
     return launch(mfa_bwd_q_fast_kernel<E, DP, BT, true>, grid, dim3(256), LDS + 128, stream, q);
   return launch(mfa_bwd_q_fast_kernel<E, DP, BT>, grid, dim3(256), LDS, stream, q);
@@ -1030,8 +963,6 @@ namespace mfa {
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I8>(BwdParams); \
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I4>(BwdParams); \
   template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, true>(BwdParams);   \
-  template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, false, SRC_I8>(BwdParams); \
-  template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, false, SRC_I4>(BwdParams); \
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_SAME, true>(BwdParams);
 MFA_BF_INST(F16, 64)
 MFA_BF_INST(F16, 128)

@@ -1108,10 +1108,8 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
   if (phase & PHASE_QUERY) {
     p.nblk = (p.R + bp - 1) / bp;
     if (p.R > 0) {
-      // Quantised K/V with 16-bit Q: the tuned kernel widens them on the way to LDS.
-      const bool fast_q = fast || (!big && ksrc > 0 && bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true));
-      hipError_t e = big      ? mfa::bwd_bigd_dispatch(p, 0, elem, stream)
-                     : fast_q ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream)
+      hipError_t e = big    ? mfa::bwd_bigd_dispatch(p, 0, elem, stream)
+                     : fast ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream)
                             : hipErrorNotSupported;
       if (big && e == hipErrorNotSupported)
         return fail(MFA_ERR_UNSUPPORTED, "head dimension %d: mixed operand precisions", p.D);
@@ -1294,12 +1292,11 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   p.dk_mul = fq;
   if ((st = plan_masks(base, nullptr, R, C, &p.mask)) != MFA_SUCCESS) return st;
   int ksrc = src_kind(kp), qsrc = src_kind(qp);
-  // backwardKeyValue or backwardQuery alone with 16-bit Q: the key phase reads each key
-  // block's K/V rows once per workgroup into registers and widens them there; the query phase
-  // widens each K/V tile on its way to LDS.  The pass would only add traffic (MFA_KV_REGS=0
-  // keeps the pass: A/B, bit-identity tests).
+  // backwardKeyValue alone with 16-bit Q: its kernel reads each key block's K/V rows once per
+  // workgroup into registers and widens them there, so the pass would only add traffic
+  // (MFA_KV_REGS=0 keeps the pass: A/B, bit-identity tests).
   const char* kvr = getenv("MFA_KV_REGS");
-  const bool kv_regs = phase != PHASE_BOTH && ksrc > 0 && qsrc == 0 && !(kvr && kvr[0] == '0') &&
+  const bool kv_regs = phase == PHASE_KV && ksrc > 0 && qsrc == 0 && !(kvr && kvr[0] == '0') &&
                        !dequant_pass_needed(D) &&
                        bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true);
   if (dequant_pass_worth(R, H, Hkv, D, elem) && !kv_regs) {

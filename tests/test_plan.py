@@ -61,7 +61,7 @@ def test_c5_forward_and_backward_phases():
     assert f["name"] == "mfa_fwd2_share_kernel<F16, 256, 32, false, false, false, false>"
     q = one(mfa.multihead_plan(d, K.backwardQuery))
     kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
-    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32, false, 0>"
+    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32, false>"
     assert kv["name"] == "mfa_bwd_kv_fast_kernel<F16, 256, 32, 0, false>"
     assert q["workgroups"] == 32 * 8 * 32 and kv["workgroups"] == 32 * 8 * 32
     for r in (f, q, kv):
@@ -101,10 +101,10 @@ def test_quantized_plans():
     # it stages them (attention_fwd_kv8.hip), no pass.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
     assert [r["name"] for r in mfa.quantized_plan(qx)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, 1, 3, 12, 14>"]
-    # backwardQuery: the tuned kernel widens each quantised K/V tile on its way to LDS
-    # (SRC_I8 = 1), no pass.
-    assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardQuery)] == \
-        ["mfa_bwd_q_fast_kernel<F16, 128, 64, false, 1>"]
+    # backwardQuery: one dequantisation pass per quantised operand (kv_dequant.hip), then the
+    # tuned 16-bit kernel on the dense copies (K/V tiles stream through LDS).
+    assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardQuery)][2] == \
+        "mfa_bwd_q_fast_kernel<F16, 128, 64, false>"
     # backwardKeyValue reads each key block's K/V once into registers and widens them there:
     # the INT8 instantiation (SRC_I8 = 1), no pass.
     assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardKeyValue)] == \
