@@ -402,12 +402,6 @@ hipError_t launch_bwd_kv(const BwdParams& p, hipStream_t stream) {
   constexpr int TILEB = A::is_f32 ? BT * (DP + 1) * 4 : BT * DP * 2;
   constexpr int LDS = 4 * TILEB + 4 * BT * 4;
   constexpr int DC = DP >= 256 ? (A::is_f32 ? 64 : 128) : DP;  // dK/dV columns per workgroup
-  if constexpr (DC != DP) {
-    const char* e = getenv("MFA_BWD256_SPLIT");  // development A/B: 0 = unsplit kernel
-    if (e && e[0] == '0')
-      return launch(mfa_bwd_kv_kernel<A, DP, BT, NW, QSRC>, dim3(p.nblk * p.B * p.Hkv),
-                    dim3(NW * 64), LDS, stream, p);
-  }
   auto kern = mfa_bwd_kv_kernel<A, DP, BT, NW, QSRC, DC>;
   return launch(kern, dim3(p.nblk * p.B * p.Hkv, DP / DC), dim3(NW * 64), LDS, stream, p);
 }

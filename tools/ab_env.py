@@ -97,6 +97,26 @@ def workload(name, dev="cuda:0"):
                      stream=stream)
         return (lambda: mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf, mask=mask,
                                      phase="keyValue", stream=stream)), 8.0 * B * H * S * S * D
+    if name in ("qbwdq256", "qbwdq128"):
+        # QuantizedAttention.backwardQuery, INT8 K/V per-tensor + fp16 Q/dO, B2 H32 S4096.
+        B, H, S, D = 2, 32, 4096, int(name[5:])
+        q, do = (u((B, H, S, D), torch.float16) for _ in range(2))
+        kf, vf = u((B, H, S, D), torch.float32), u((B, H, S, D), torch.float32)
+        kq, ks, _, _ = mfa.quantize(kf, mfa.Precision.INT8, rows=B * H * S, cols=D)
+        vq, vs, _, _ = mfa.quantize(vf, mfa.Precision.INT8, rows=B * H * S, cols=D)
+        base = mfa.AttentionDescriptor.make(S, S, D, low_precision=True, precision=mfa.Precision.FP16)
+        qd = mfa.quantized_descriptor(base, mfa.Precision.FP16, mfa.Precision.INT8, mfa.Precision.INT8, B=B, H=H)
+        tq = mfa.quantized_tensor(q, mfa.Precision.FP16)
+        tk = mfa.quantized_tensor(kq, mfa.Precision.INT8, scale=float(ks.item()))
+        tv = mfa.quantized_tensor(vq, mfa.Precision.INT8, scale=float(vs.item()))
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
+        dq = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+        dvals = torch.empty((B, H, S), dtype=torch.bfloat16, device=dev)
+        qa = mfa.QuantizedAttention()
+        qa.forward(qd, tq, tk, tv, o, l, stream=stream)
+        return (lambda: qa.backwardQuery(qd, tq, tk, tv, o, do, l, dq, dvals, stream=stream)), \
+            6.0 * B * H * S * S * D
     raise SystemExit(f"unknown workload {name}")
 
 
