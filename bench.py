@@ -404,6 +404,22 @@ def main():
         ms_dn = ev_time(lambda: mha.forward(desc_d, qs, ks_, vs_, os_, ls, stream=stream))
         pairs = int((rows[0, 0, :, 1].astype(np.int64) - rows[0, 0, :, 0]).sum()) * B * Hs
         fs = 4.0 * Ds * pairs
+        # Backward on the same ranges (both phases; the tuned kernels' mask instantiation skips
+        # the key tiles / steps no row of a block sees) against the dense backward.
+        dos = uniform((B, Hs, Ss, Ds), torch.float16)
+        dqs = torch.empty((B, Hs, Ss, Ds), dtype=torch.float32, device=dev)
+        dks, dvs = torch.empty_like(dqs), torch.empty_like(dqs)
+        dbs = torch.empty((B, Hs, Ss), dtype=torch.bfloat16, device=dev)
+        mha.forward(desc_s, qs, ks_, vs_, os_, ls, mask=mask_s, stream=stream)
+        bw_sp = ev_time(lambda: mha.backward(desc_s, qs, ks_, vs_, os_, dos, ls, dqs, dks, dvs, dbs,
+                                             mask=mask_s, stream=stream))
+        mfa.last_launches()
+        mha.backward(desc_s, qs, ks_, vs_, os_, dos, ls, dqs, dks, dvs, dbs, mask=mask_s,
+                     stream=stream)
+        plan_bs = [r["name"] for r in mfa.last_launches()]
+        mha.forward(desc_d, qs, ks_, vs_, os_, ls, stream=stream)
+        bw_dn = ev_time(lambda: mha.backward(desc_d, qs, ks_, vs_, os_, dos, ls, dqs, dks, dvs, dbs,
+                                             stream=stream))
         result["block_sparse"] = {
             "workload": f"sparse ranges from buildBlockSparse, fp16 B{B} H{Hs} S{Ss} D{Ds}, "
                         f"{blk}x{blk} blocks, band of {band} key blocks per row block "
@@ -413,8 +429,13 @@ def main():
             "ms": round(ms_sp, 4), "dense_ms": round(ms_dn, 4),
             "speedup_vs_dense": round(ms_dn / ms_sp, 2),
             "kernels": plan_s,
+            "bwd_tflops_on_kept_pairs": round(2.5 * fs / (bw_sp * 1e-3) / 1e12, 2),
+            "bwd_flop_convention": "10*D per kept pair (the 7-GEMM backward executes 14*D)",
+            "bwd_ms": round(bw_sp, 4), "bwd_dense_ms": round(bw_dn, 4),
+            "bwd_speedup_vs_dense": round(bw_dn / bw_sp, 2),
+            "bwd_kernels": plan_bs,
         }
-        del qs, ks_, vs_, os_, ls, mask_s
+        del qs, ks_, vs_, os_, ls, mask_s, dos, dqs, dks, dvs, dbs
 
     # ------------------------------------------------- SURVEY §8(f) rows (one GPU's view)
     if not args.no_next:

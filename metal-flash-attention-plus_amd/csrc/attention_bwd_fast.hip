@@ -489,6 +489,45 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     const int64_t hi = (int64_t)k0 + BK + (int64_t)p.mask.window_size;
     if (hi < qend) qend = (int)hi;
   }
+  if constexpr (MSK) {
+    // The rows that see this key block (their unmasked interval meets [k0, k0 + BK)) or sit at
+    // the mask level (no unmasked key: they see every key): the query tiles run from the first
+    // to the last of them only (the intervals are the same for every head of the kv group).
+    // A pre-pass over the rows' intervals, one row per thread per 256.
+    int rmin = p.R, rmax = -1;
+#pragma unroll 8
+    for (int q = tid; q < p.R; q += NT) {
+      int64_t lo = 0, hi = p.C;
+      if (p.mask.ranges) {
+        const uint2 r = *reinterpret_cast<const uint2*>(
+            p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + q));
+        lo = r.x;
+        hi = min((int64_t)r.y, (int64_t)p.C);
+      }
+      if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
+      if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
+      if (lo >= hi || (lo < k0 + BK && hi > k0)) {
+        rmin = min(rmin, q);
+        rmax = max(rmax, q);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      rmin = min(rmin, __shfl_xor(rmin, o));
+      rmax = max(rmax, __shfl_xor(rmax, o));
+    }
+    int* red = reinterpret_cast<int*>(smem);  // before any tile lands in LDS
+    if (lane == 0) { red[wave * 2] = rmin; red[wave * 2 + 1] = rmax; }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      rmin = min(rmin, red[w * 2]);
+      rmax = max(rmax, red[w * 2 + 1]);
+    }
+    __syncthreads();
+    qbeg = max(qbeg, (rmin / BQ) * BQ);
+    qend = min(qend, rmax + 1);
+  }
   const int ntile = qbeg < qend ? (qend - qbeg + BQ - 1) / BQ : 0;
   const int ngroup = (p.H - kvh + p.Hkv - 1) / p.Hkv;  // query heads h = kvh + g*Hkv
   const int nsteps = ntile * ngroup;
