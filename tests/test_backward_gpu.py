@@ -275,3 +275,28 @@ def test_masked_backward_fully_masked_rows_match_generic(gpu, monkeypatch):
                        ranges=ranges)
     e = maxerr(fast["dQ"][:, :, ~empty], ref["dQ"][:, :, ~empty])
     assert e <= 5e-2, f"dQ max error {e} on rows with keys"
+
+
+@pytest.mark.parametrize("D,prec", [(128, FP16), (64, BF16), (256, FP16)])
+def test_block_sparse_backward_skips_match_oracle(gpu, D, prec):
+    # buildBlockSparse ranges (SparseMQABuilder.swift:30-62) over many key blocks: the query
+    # phase bounds its key tiles by the block's union, the key phase runs only the query tiles
+    # whose rows see its key block and skips steps none sees.  Banded pattern with a ragged
+    # per-row-block width, GQA group of 2, R != C.
+    B, H, Hkv, R, C, blk = 1, 4, 2, 640, 768, 64
+    nbr, nbc = R // blk, C // blk
+    rng = np.random.default_rng(90 + D)
+    pat = np.zeros((nbr, nbc), dtype=np.uint8)
+    for i in range(nbr):
+        w = int(rng.integers(1, 5))
+        c0 = int(rng.integers(0, nbc - w + 1))
+        pat[i, c0:c0 + w] = 1
+    rb = np.zeros((nbr, 2), dtype=np.uint32)
+    mfa.lib.mfa_sparse_build_block_sparse(pat.ctypes.data, nbr, nbc, blk, rb.ctypes.data)
+    ranges = np.ascontiguousarray(np.broadcast_to(np.repeat(rb, blk, axis=0), (B, Hkv, R, 2)))
+    Q, dO = gaussian((B, H, R, D), 91) * 0.5, gaussian((B, H, R, D), 92) * 0.5
+    K, V = gaussian((B, Hkv, C, D), 93) * 0.5, gaussian((B, Hkv, C, D), 94) * 0.5
+    mfa.last_launches()
+    check_backward(Q, K, V, dO, prec, 5e-2, 1e-1, ranges=ranges)
+    names = [x["name"] for x in mfa.last_launches()]
+    assert any(n.startswith("mfa_bwd_kv_fast_kernel") and n.endswith("true>") for n in names), names
