@@ -301,9 +301,13 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
   // MSK: a row at the mask level (every key masked) takes the rounded product S·c before
   // subtracting L, as the generic kernel does (attention_bwd.h).
-  const bool lmask = MSK && Lrow < kMaskLevel;
+  // MSK takes the rounded product for every row (two VALU, no per-lane select): exact for
+  // rows at the mask level, within rounding of the fused form elsewhere.
   auto pexp = [&](float x) {
-    return __builtin_amdgcn_exp2f(lmask ? mul_rn(x, c) - Lrow : __builtin_fmaf(x, c, -Lrow));
+    if constexpr (MSK)
+      return __builtin_amdgcn_exp2f(mul_rn(x, c) - Lrow);
+    else
+      return __builtin_amdgcn_exp2f(__builtin_fmaf(x, c, -Lrow));
   };
 
   f32x16 dq[ND];
@@ -330,22 +334,30 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     // element (j, i) is key t + 32j + 8(i>>2) + 4hh + (i&3) of this lane's row.
     float am[MSK ? NJ : 1][16];
     if constexpr (MSK) {
-      const float* arow = p.mask.amask + row * p.C;
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = t + 32 * j + 8 * (i >> 2) + 4 * hh + (i & 3);
-          am[j][i] = (p.mask.amask && qvalid && key < p.C) ? arow[key] : 0.f;
-        }
+        for (int i = 0; i < 16; ++i) am[j][i] = 0.f;
+      if (p.mask.amask) {  // wave-uniform: no per-element branch without an additive mask
+        const float* arow = p.mask.amask + row * p.C;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = t + 32 * j + 8 * (i >> 2) + 4 * hh + (i & 3);
+            if (qvalid && key < p.C) am[j][i] = arow[key];
+          }
+      }
     }
     rows_chain<A, NJ>(kt, qf, s, rbase, [](int) {});
     if constexpr (MSK) {
       if (t >= tin_lo && min(t + BT, p.C) <= tin_hi) {
+        if (p.mask.amask) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
+          for (int j = 0; j < NJ; ++j)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) s[j][i] += am[j][i];
+            for (int i = 0; i < 16; ++i) s[j][i] += am[j][i];
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)

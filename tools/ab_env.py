@@ -77,8 +77,9 @@ def workload(name, dev="cuda:0"):
         # per tile.
         B, H, S, D = 1, 16, 2048, int(name[3:6])
         q, k, v, do = (u((B, H, S, D), torch.float16) for _ in range(4))
-        mask = u((B, H, S, S), torch.float32) if name.endswith("_amask") else None
-        if name.endswith("_ranges"):  # every key in range: the mask path with no amask traffic
+        name_ = name[:-2] if name.endswith("_q") else name
+        mask = u((B, H, S, S), torch.float32) if name_.endswith("_amask") else None
+        if name_.endswith("_ranges"):  # every key in range: the mask path with no amask traffic
             import numpy as np
             rows = np.zeros((B, H, S, 2), dtype=np.uint32)
             rows[..., 1] = S
@@ -89,14 +90,16 @@ def workload(name, dev="cuda:0"):
         dq, dk, dv = (torch.empty((B, H, S, D), dtype=torch.float32, device=dev) for _ in range(3))
         base = mfa.AttentionDescriptor.make(
             low_precision=True, precision=mfa.Precision.FP16,
-            sparse_mask=mfa.MaskType.sparseRanges if name.endswith("_ranges") else None)
+            sparse_mask=mfa.MaskType.sparseRanges if name_.endswith("_ranges") else None)
         desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
         mha = mfa.MultiHeadAttention()
         mha.forward(desc, q, k, v, o, l, mask=mask, stream=stream)
         mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf, mask=mask, phase="query",
                      stream=stream)
+        ph = "query" if name.endswith("_q") else "keyValue"  # *_q: the query phase (3 GEMMs)
         return (lambda: mha.backward(desc, q, k, v, o, do, l, dq, dk, dv, dbuf, mask=mask,
-                                     phase="keyValue", stream=stream)), 8.0 * B * H * S * S * D
+                                     phase=ph, stream=stream)), \
+            (6.0 if ph == "query" else 8.0) * B * H * S * S * D
     if name in ("qbwdq256", "qbwdq128"):
         # QuantizedAttention.backwardQuery, INT8 K/V per-tensor + fp16 Q/dO, B2 H32 S4096.
         B, H, S, D = 2, 32, 4096, int(name[5:])
