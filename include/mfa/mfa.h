@@ -303,8 +303,11 @@ typedef enum mfa_quantization_strategy {
  * For FP16/BF16/FP32 precisions the quantization fields are ignored. `data` is a device
  * pointer to the contiguous [B, H, S, D] tensor (INT4: two values per byte, element 2i in
  * the low nibble of byte i, GEMMQuantization.swift:500-515).  Blockwise scales are
- * device arrays indexed (row / bs) * ceil(D / bs) + col / bs over the 2-D view
- * [B*H*S, D] (GEMMQuantization.swift:561-575). */
+ * device arrays indexed (row / bs) * ceil(cols / bs) + col / bs over the tensor's 2-D memory
+ * view (GEMMQuantization.swift:561-575): [B*H*S rows, D cols] for a row-major operand, and
+ * [B*H*D rows, S cols] for one the descriptor's transposeState marks transposed (row = head
+ * dimension index, col = sequence index, as AttentionKernel+Accumulate.swift:461-472 and
+ * AttentionKernel+OuterProduct.swift:301-316 index it). */
 typedef struct mfa_quantized_tensor {
   const void* data;
   int32_t precision;           /* mfa_precision_t */
@@ -362,9 +365,11 @@ mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* desc,
  * handed to that forward is then target-quantized, as in the reference).  A target that needs
  * no quantization parameters (FP16 / BF16 / FP32) wraps the buffers as they are (:425-441).
  * Tensor-wise scales are read back to the host before the forward (one synchronisation of
- * `stream`; the reference computes them on the CPU, :479-498); blockwise scales stay on the
- * device and the call stays asynchronous.  Row-wise mode is not an attention input layout:
- * MFA_ERR_UNSUPPORTED. */
+ * `stream`; the reference computes them on the CPU, :479-498), so tensor-wise mode on a stream
+ * under graph capture returns MFA_ERR_UNSUPPORTED; blockwise scales stay on the device and the
+ * call stays asynchronous.  Each buffer is quantised as its memory view (transposed operands
+ * as [D][S] rows, see mfa_quantized_tensor_t).  Row-wise mode is not an attention input
+ * layout: MFA_ERR_UNSUPPORTED. */
 mfa_status_t mfa_quantized_forward_from_float(const mfa_quantized_descriptor_t* desc,
                                               const void* query, const void* key,
                                               const void* value, int32_t query_precision,

@@ -356,7 +356,7 @@ void decode_layout(int B, int Hkv, int rows, int C, int* nrt, int* nsplit, int* 
 // Partials workspace of the split path; 0 when a unit's keys fit one split and the workgroup
 // merges its waves' partials in LDS (the kernel then never touches the workspace).
 static bool decode_fused(int nsplit) {
-  const char* mv = getenv("MFA_DECODE_MERGE");  // =1: the separate merge pass for one split too
+  const char* mv = mfa::dev_env("MFA_DECODE_MERGE");  // =1: the separate merge pass for one split too
   return nsplit == 1 && !(mv && mv[0] == '1');
 }
 

@@ -362,11 +362,11 @@ static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
 // measured +2 % over 64-key tiles at 3 waves per SIMD (165 VGPRs) at C3 (1616-1622 vs
 // 1584-1589 TOPS, two one-process A/B runs); MFA_I8_BK=64 selects the latter.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) {
-  const char* bk = getenv("MFA_I8_BK");
+  const char* bk = mfa::dev_env("MFA_I8_BK");
   const bool small = bk && bk[0] == '6';
   // Unmasked, at least a full wave of block pairs: adjacent blocks share the staged tiles
   // (MFA_I8_SHARE=0 keeps one 4-wave workgroup per block, =1 shares at any size: tests).
-  const char* sh = getenv("MFA_I8_SHARE");
+  const char* sh = mfa::dev_env("MFA_I8_SHARE");
   if (!small && !p.mask.causal && !p.mask.window &&
       (sh ? sh[0] == '1'
           : (p.nblk % 2 == 0 || p.nblk >= 8) && (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256)) {

@@ -190,7 +190,7 @@ hipError_t fwd_kv8_dispatch(const FwdParams& p, int elem, int src, hipStream_t s
   const dim3 grid(npairs * p.B * p.H);
   const size_t lds = fwd_kv8_lds_bytes();
   // MFA_KV8_SLOTS=1 (development A/B): the widening pieces at QK^T MFMAs 4 / 10 and PV 4 / 10.
-  const char* sl = getenv("MFA_KV8_SLOTS");
+  const char* sl = mfa::dev_env("MFA_KV8_SLOTS");
   const bool alt = sl && sl[0] == '1';
   if (src == SRC_I8)
     return alt ? launch(mfa_fwd2_kv8_kernel<F16, 128, 64, SRC_I8, 4, 10, 4, 10>, grid, dim3(512), lds, stream, q)

@@ -426,7 +426,7 @@ static int stream_grid() {
       n = 256;
     return n;
   }();
-  if (const char* e = getenv("MFA_FWD_STREAM_WGS")) {
+  if (const char* e = mfa::dev_env("MFA_FWD_STREAM_WGS")) {
     const int n = atoi(e);
     if (n > 0) return n;
   }
@@ -437,11 +437,11 @@ static int stream_grid() {
 // stream kernel.
 static bool stream_split(const FwdParams& p, int elem, int DP, int* W, int* L, int* T, int* Th,
                          int* nb) {
-  const char* e = getenv("MFA_FWD_STREAM");
+  const char* e = mfa::dev_env("MFA_FWD_STREAM");
   if (e && e[0] == '0') return false;
   const bool force = e && e[0] == '1';
   // The other causal kernels' A/B switches keep those kernels.
-  if (!force && (getenv("MFA_FWD_VARIANT") || getenv("MFA_FWD_PAIR"))) return false;
+  if (!force && (mfa::dev_env("MFA_FWD_VARIANT") || mfa::dev_env("MFA_FWD_PAIR"))) return false;
   if (!p.mask.causal || p.mask.window || p.mask.ranges || p.mask.amask) return false;
   if ((elem != P_FP16 && elem != P_BF16) || (DP != 64 && DP != 128)) return false;
   constexpr int BK = 64;
@@ -489,7 +489,7 @@ hipError_t fwd_stream_dispatch(const FwdParams& p0, int elem, int DP, hipStream_
   p.sk_cnt_bytes = (int)(((size_t)p.B * p.H * nb * 4 + 255) / 256 * 256);
   // Tests: MFA_FWD_STREAM_SLOW=1 makes every closer publish and count in (the merge then
   // runs from the workspace in whichever workgroup counts in last).
-  const char* sl = getenv("MFA_FWD_STREAM_SLOW");
+  const char* sl = mfa::dev_env("MFA_FWD_STREAM_SLOW");
   p.sk_flags = sl && sl[0] == '1' ? 1 : 0;
   auto lds = [](int dp) { return 4 * 64 * dp * 2 + 128 * (dp * 4 + 16) + 16; };  // ring, image, flag
 #define MFA_FS(ELEM, EE, DPV)                                                              \

@@ -7,8 +7,8 @@
 // sliding-window masks whose fully masked tiles may be skipped (so no row is masked
 // everywhere).  The host routes everything else to the other kernels.
 //
-// What is different from attention_fwd_fast.hip, all aimed at the VALU work per MFMA (the
-// binding limit of that kernel):
+// What is different from the first-generation forward (attention_fwd_fast.hip, removed in round
+// 5), all aimed at the VALU work per MFMA (the binding limit of that kernel):
 //   * K/V tiles land by LDS-DMA in the sub-tiled TileA image, so every fragment read is a base
 //     register plus an immediate (no per-read address arithmetic);
 //   * fp16: Q is pre-scaled by c = scale·log2(e) in registers and the first QK^T MFMA of each
@@ -841,18 +841,18 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   q.nblk = (p.R + 127) / 128;
   const int npairs = (q.nblk + 1) / 2;
   {
-    const char* xh = getenv("MFA_SHARE_XCD");  // A/B: 0 deals pairs round-robin over heads
+    const char* xh = mfa::dev_env("MFA_SHARE_XCD");  // A/B: 0 deals pairs round-robin over heads
     q.xcd_heads = !(xh && xh[0] == '0');
   }
   // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
   // (A/B).
   // Mirrored pairs: deferred V0 (+1.2 % at C2 in one-process A/B) and non-temporal O image
   // stores by default; MFA_SHARE_DV=0 / MFA_SHARE_NT=0 turn them off (A/B).
-  const char* dvv = getenv("MFA_SHARE_DV");
-  const char* nt = getenv("MFA_SHARE_NT");
+  const char* dvv = mfa::dev_env("MFA_SHARE_DV");
+  const char* nt = mfa::dev_env("MFA_SHARE_NT");
   // ... and A's O at the switch leaves through the wave's Q staging region as whole
   // half-rows (+0.8 % at C2; MFA_SHARE_SWI=0 keeps row-per-lane stores there).
-  const char* swi = getenv("MFA_SHARE_SWI");
+  const char* swi = mfa::dev_env("MFA_SHARE_SWI");
   if (MIRROR && !(dvv && dvv[0] == '0') && !(nt && nt[0] == '0')) {
     if (swi && swi[0] == '0')
       return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, false, true>,
@@ -864,7 +864,7 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
     // Adjacent pairs (D <= 128): both blocks leave through O row images by non-temporal
     // whole-row stores (C3 +0.8 %, C4's attention +1.9 % in one-process A/B; plain stores
     // from the images: +0.5 / +0.9 %).  MFA_SHARE_IMG=0 keeps row-per-lane stores (A/B).
-    const char* im = getenv("MFA_SHARE_IMG");
+    const char* im = mfa::dev_env("MFA_SHARE_IMG");
     if (!(im && im[0] == '0'))
       return launch(mfa_fwd2_share_kernel<E, DP, BK, MIRROR, true, true>,
                     dim3(npairs * p.B * p.H), dim3(512), LDS_IMG, stream, q);
@@ -903,13 +903,7 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
 
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream) {
-  const char* var = getenv("MFA_FWD_VARIANT");
-  if (const char* aw = getenv("MFA_FWD_AW")) {
-    if (aw[0] == '1') {
-      const hipError_t e = fwd_aw_dispatch(p, elem, DP, stream);
-      if (e != hipErrorNotSupported) return e;
-    }
-  }
+  const char* var = mfa::dev_env("MFA_FWD_VARIANT");
   const int blocks = p.nblk * p.B * p.H;
   // Causal: mirrored pairs while they fill at most ~1.5 rounds of the chip, or up to 3 rounds
   // for long rows (S >= 8192: 64 blocks; one-process A/B: H16 S8192 1057 vs 987 TF single,
@@ -919,7 +913,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   if (var && var[0] == 's') single = true;
   if (var && var[0] == 'p' && !p.mask.ranges) single = false;
   // Development A/B of the scheduling knobs on the fp16 D=128 single-block kernel.
-  if (const char* tv = getenv("MFA_FWD2_TUNE")) {
+  if (const char* tv = mfa::dev_env("MFA_FWD2_TUNE")) {
     if (elem == P_FP16 && DP == 128 && single) {
       switch (tv[0]) {
         case '1': return launch_fwd2<F16, 128, 64, 2, Tune<8, 4>>(p, stream);
@@ -932,7 +926,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
       }
     }
   }
-  const char* pv = getenv("MFA_FWD_PAIR");
+  const char* pv = mfa::dev_env("MFA_FWD_PAIR");
   const bool pair64 = pv && pv[0] == '2';
   // Causal pairs run the shared-tile schedule; MFA_FWD_PAIR=o keeps the pair kernel (A/B).
   const bool share = !(pv && (pv[0] == 'o' || pv[0] == '2' || pv[0] == 'n')) && !p.mask.window;
@@ -942,7 +936,7 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
   // K/V tile (256 query rows per staged tile; +6.5 % at C3 over the single-block kernel).
   // MFA_FWD_SHARE=0 keeps the single-block kernel (A/B), =1 takes the shared-tile kernel at
   // any size (tests).
-  const char* sv = getenv("MFA_FWD_SHARE");
+  const char* sv = mfa::dev_env("MFA_FWD_SHARE");
   // (An odd block count leaves group 1 of the last pair without rows: not for nblk < 8 odd.)
   // Sparse ranges take the adjacent pairs too (D <= 128): the pair stages the union of its
   // blocks' key ranges and each group computes its own (MFA_FWD_SHARE=0 keeps the single-block

@@ -344,7 +344,7 @@ static hipError_t launch_gemm2(const GemmParams& p0, int batch, hipStream_t stre
   const dim3 grid(p0.N / 128, p0.M / 128, batch);
   // Whole-row C stores need 16-B aligned rows; MFA_GEMM_IMG=0 keeps the per-lane stores (A/B).
   GemmParams p = p0;
-  const char* ie = getenv("MFA_GEMM_IMG");
+  const char* ie = mfa::dev_env("MFA_GEMM_IMG");
   auto al16 = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
   p.c_img = p.prec_c != P_FP32 && (p.ldc & 7) == 0 && (p.b[1] || (p.sc & 7) == 0) &&
             al16(p.c[0]) && al16(p.c[1]) && !(ie && ie[0] == '0');
@@ -352,7 +352,7 @@ static hipError_t launch_gemm2(const GemmParams& p0, int batch, hipStream_t stre
   if (p.trans_a) return launch(mfa_gemm2_kernel<E, 2>, grid, dim3(256), LDS, stream, p);
   // NN in the natural k order (4096^3 fp16: 856-959 vs 745-749 TF for the permuted order;
   // C4 151.3 vs 153.1 us).  MFA_GEMM_NN=0 keeps the permuted-order kernel (A/B).
-  const char* nn = getenv("MFA_GEMM_NN");
+  const char* nn = mfa::dev_env("MFA_GEMM_NN");
   if (nn && nn[0] == '0') return launch(mfa_gemm2_kernel<E, 0>, grid, dim3(256), LDS, stream, p);
   return launch(mfa_gemm2_kernel<E, 3>, grid, dim3(256), LDS, stream, p);
 }
@@ -526,7 +526,7 @@ static hipError_t launch_gemm3(const GemmParams& p0, int batch, hipStream_t stre
 }
 
 static bool gemm2_eligible(const GemmParams& p) {
-  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+  if (const char* e = mfa::dev_env("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return false;
   }
   if (p.M % 128 || p.N % 128 || p.K % 64 || p.K == 0 || p.load_prev) return false;
@@ -548,7 +548,7 @@ static bool gemm2_eligible(const GemmParams& p) {
 // win, e.g. a single [4096, 512] x [512, 2048] 15.0 vs 20.1 us).  MFA_GEMM3=0 / =1 forces
 // gemm2 / gemm3 (A/B, tests).
 static bool gemm3_pick(const GemmParams& p, int batch) {
-  const char* g3 = getenv("MFA_GEMM3");
+  const char* g3 = mfa::dev_env("MFA_GEMM3");
   const int64_t tiles3 = (int64_t)(p.M / 256) * (p.N / 256) * batch;
   return p.M % 256 == 0 && p.N % 256 == 0 && (g3 ? g3[0] == '1' : tiles3 >= kGemm3MinTiles);
 }

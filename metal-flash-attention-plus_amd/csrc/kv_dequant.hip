@@ -29,8 +29,8 @@ __global__ void __launch_bounds__(256) mfa_kv_dequant_kernel(Operand op, int Hx,
     const int64_t rowoff = (int64_t)b * op.sb + (int64_t)hx * op.sh + (int64_t)row * op.ss;
     const int d0 = c * 8;
     const uint4 raw = load_qchunk<SRC>(op, rowoff, d0, D);
-    const uint4 v = convert_qchunk<E, SRC>(raw, op, op.bscale ? quant_row(op, b, hx, row) : 0, d0, D,
-                                           true);
+    const uint4 v = convert_qchunk<E, SRC>(raw, op, op.bscale ? quant_row(op, b, hx) : 0, row, d0,
+                                           D, true);
     uint16_t* dst = out + rowg * D + d0;
     if (d0 + 8 <= D) {
       *reinterpret_cast<uint4*>(dst) = v;

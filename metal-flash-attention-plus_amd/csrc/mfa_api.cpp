@@ -100,31 +100,42 @@ struct ScratchKey {
     return slot < o.slot;
   }
 };
+struct ScratchBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  size_t zeroed = 0;  // leading bytes known to be zero (arrival counters every launch resets)
+};
 struct Scratch {
   std::mutex mu;
-  std::map<ScratchKey, std::pair<void*, size_t>> bufs;
+  std::map<ScratchKey, ScratchBuf> bufs;
 } g_scratch;
 
-// zero_bytes: the first bytes of a newly allocated buffer are zeroed (stream-ordered), e.g.
-// arrival counters that every launch leaves at zero.
+// zero_bytes: the first bytes of the buffer must be zero when the call's kernel starts, e.g.
+// arrival counters that every launch leaves at zero.  The zeroed prefix is tracked per buffer:
+// a call whose counter region is longer than the previous call's (a different shape in the
+// same buffer) zeroes it again, since the bytes past the old prefix hold partial states.
 mfa_status_t scratch(size_t bytes, void** out, int slot, hipStream_t stream, size_t zero_bytes = 0) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(MFA_ERR_NO_DEVICE, "no HIP device");
   std::lock_guard<std::mutex> lock(g_scratch.mu);
   auto& b = g_scratch.bufs[ScratchKey{dev, stream, slot}];
-  if (b.second < bytes) {
-    if (b.first) (void)hipFreeAsync(b.first, stream);
-    b = {nullptr, 0};
+  if (b.bytes < bytes) {
+    if (b.ptr) (void)hipFreeAsync(b.ptr, stream);
+    b = ScratchBuf();
     void* p = nullptr;
     hipError_t e = hipMallocAsync(&p, bytes, stream);
     if (e != hipSuccess) return hip_status(e, "hipMallocAsync(scratch)");
-    if (zero_bytes && (e = hipMemsetAsync(p, 0, zero_bytes, stream)) != hipSuccess) {
-      (void)hipFreeAsync(p, stream);
-      return hip_status(e, "hipMemsetAsync(scratch)");
-    }
-    b = {p, bytes};
+    b.ptr = p;
+    b.bytes = bytes;
   }
-  *out = b.first;
+  if (zero_bytes > b.zeroed) {
+    const hipError_t e = hipMemsetAsync(b.ptr, 0, zero_bytes, stream);
+    if (e != hipSuccess) return hip_status(e, "hipMemsetAsync(scratch)");
+  }
+  // After this call's launch only its own counter prefix is known to be zero again: the bytes
+  // behind it hold this call's partial states.
+  b.zeroed = zero_bytes;
+  *out = b.ptr;
   return MFA_SUCCESS;
 }
 
@@ -241,32 +252,10 @@ mfa_status_t plan_masks(const mfa_attention_descriptor_t& base, const void* mask
   return MFA_SUCCESS;
 }
 
-// The tuned forward kernel (attention_fwd_fast.hip) covers 16-bit operands with 16-byte aligned
-// rows (8-byte for INT8 K/V), D % 8 == 0, causal / window masks and per-tensor quantisation.
-bool fast_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
-  if (const char* e = getenv("MFA_DISABLE_FAST")) {
-    if (e[0] == '1') return false;
-  }
-  if (elem != 1 && elem != 2) return false;
-  if (kvsrc == 0 && DP != 64 && DP != 128) return false;
-  if (kvsrc == 1 && DP != 128) return false;
-  if (kvsrc > 1) return false;
-  if (p.D % 8 != 0 || p.mask.amask || p.mask.ranges) return false;
-  if (!p.q.vec || !p.k.vec || !p.v.vec) return false;
-  if (p.q.prec != (elem == 1 ? MFA_PRECISION_FP16 : MFA_PRECISION_BF16)) return false;
-  if (p.k.bscale || p.v.bscale) return false;
-  // K/V are addressed per head with 32-bit buffer offsets (attention_fwd_fast.hip KVStage).
-  const int64_t esz = kvsrc == 0 ? 2 : 1;
-  if ((int64_t)p.C * p.k.ss * esz >= ((int64_t)1 << 31) ||
-      (int64_t)p.C * p.v.ss * esz >= ((int64_t)1 << 31))
-    return false;
-  return p.q.sd == 1 && p.k.sd == 1 && p.v.sd == 1 && p.o_sd == 1;
-}
-
 // attention_fwd_v2.hip: also D = 256, but needs a positive scale and, with causal / window
 // masks, no fully masked row (skip_ok), since it masks with -inf.
 bool fwd2_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
-  if (const char* e = getenv("MFA_FWD_GEN")) {
+  if (const char* e = mfa::dev_env("MFA_FWD_GEN")) {
     if (e[0] == '1') return false;
   }
   if (elem != 1 && elem != 2) return false;
@@ -289,7 +278,7 @@ bool fwd2_eligible(const mfa::FwdParams& p, int elem, int DP, int kvsrc) {
 
 hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, hipStream_t s) {
   if (DP == kBigD) return mfa::fwd_bigd_dispatch(p, elem, s);
-  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+  if (const char* e = mfa::dev_env("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
   }
   if (fwd2_eligible(p, elem, DP, kvsrc)) {
@@ -307,10 +296,6 @@ hipError_t launch_forward(const mfa::FwdParams& p, int elem, int DP, int kvsrc, 
       }
     }
     hipError_t e = mfa::fwd2_dispatch(p, elem, DP, s);
-    if (e != hipErrorNotSupported) return e;
-  }
-  if (fast_eligible(p, elem, DP, kvsrc)) {
-    hipError_t e = mfa::fwd_fast_dispatch(p, elem, DP, kvsrc, s);
     if (e != hipErrorNotSupported) return e;
   }
   return mfa::fwd_dispatch(p, elem, DP, kvsrc, kvsrc, s);
@@ -363,8 +348,8 @@ int mfa_release_scratch(void* stream) {
   int n = 0;
   for (auto it = g_scratch.bufs.begin(); it != g_scratch.bufs.end();) {
     if (it->first.dev == dev && (!stream || it->first.stream == (hipStream_t)stream)) {
-      if (it->second.first) {
-        (void)hipFreeAsync(it->second.first, it->first.stream);
+      if (it->second.ptr) {
+        (void)hipFreeAsync(it->second.ptr, it->first.stream);
         ++n;
       }
       it = g_scratch.bufs.erase(it);
@@ -688,7 +673,12 @@ mfa_status_t quant_operand(const mfa_quantized_tensor_t* t, int cfg_prec, int B,
       op->bscale = t->block_scales;
       op->bzp = t->block_zero_points;
       op->bsize = (int)t->block_size;
-      op->bcols = (D + (int)t->block_size - 1) / (int)t->block_size;
+      // The block grid is over the memory view (AttentionKernel+Accumulate.swift:461-472):
+      // [S][D] rows, or [D][S] rows for a transposed operand (row = d, col = seq,
+      // ceil(leadingDimension / BLOCK_SIZE_K) blocks per row, leadingDimension = S).
+      op->qtr = transposed ? 1 : 0;
+      op->cols = transposed ? S : D;
+      op->bcols = (op->cols + (int)t->block_size - 1) / (int)t->block_size;
     } else {
       *fold = t->scale;
       op->zp = t->zero_point;
@@ -722,7 +712,7 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
 // K/V with the same row layout, 16-byte rows (INT4: D % 32 == 0, 16-byte packed rows), D <= 256,
 // no mask, dense O rows.
 bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
-  if (const char* e = getenv("MFA_DECODE")) {
+  if (const char* e = mfa::dev_env("MFA_DECODE")) {
     if (e[0] == '0') return false;
   }
   if (elem != 1 && elem != 2) return false;
@@ -746,7 +736,7 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
 // 16-byte aligned byte offsets.  MFA_KV8=0 routes these through the dequantisation pass
 // instead (A/B).
 bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int DP) {
-  if (const char* e = getenv("MFA_KV8")) {
+  if (const char* e = mfa::dev_env("MFA_KV8")) {
     if (e[0] == '0') return false;
   }
   if (elem != 1 || qp != MFA_PRECISION_FP16) return false;
@@ -775,7 +765,7 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
 bool dequant_pass_needed(int D) { return pad_head(D) == kBigD; }
 bool dequant_pass_worth(int R, int H, int Hkv, int D, int elem) {
   if (dequant_pass_needed(D)) return true;
-  if (const char* e = getenv("MFA_NO_DEQUANT_PASS")) {
+  if (const char* e = mfa::dev_env("MFA_NO_DEQUANT_PASS")) {
     if (e[0] == '1') return false;
   }
   return (elem == 1 || elem == 2) && D % 8 == 0 && D <= 256 && (int64_t)R * (H / Hkv) >= 128;
@@ -947,17 +937,38 @@ extern "C" mfa_status_t mfa_quantized_forward_from_float(
   if (!query || !key || !value || !output)
     return fail(MFA_ERR_INVALID_ARGUMENT, "null Q / K / V / output");
   hipStream_t s = (hipStream_t)stream;
-  const uint64_t rows[3] = {(uint64_t)B * H * R, (uint64_t)B * Hkv * C, (uint64_t)B * Hkv * C};
+  if (mode == MFA_QUANT_TENSOR_WISE && !mfa::plan_capture()) {
+    // Tensor-wise scales are read back to the host between quantising and the forward (one
+    // stream synchronisation), which a stream under graph capture cannot do.
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(MFA_ERR_UNSUPPORTED,
+                  "tensor-wise runtime quantization synchronises the stream: not under graph "
+                  "capture (blockwise mode keeps its scales on the device)");
+  }
+  // Each buffer is quantised as its memory view (GEMMQuantization.swift:561-575): [S][D] rows
+  // per head, or [D][S] for a transposed operand (AttentionDescriptor transposeState), so the
+  // blockwise grid is the one the forward indexes (quant_operand).
+  const bool tr[3] = {base.has_transpose_state && base.transpose_q,
+                      base.has_transpose_state && base.transpose_k,
+                      base.has_transpose_state && base.transpose_v};
+  const uint64_t seq[3] = {R, C, C};
+  const uint64_t heads[3] = {(uint64_t)B * H, (uint64_t)B * Hkv, (uint64_t)B * Hkv};
+  uint64_t rows[3], cols[3];
+  for (int i = 0; i < 3; ++i) {
+    rows[i] = heads[i] * (tr[i] ? D : seq[i]);
+    cols[i] = tr[i] ? seq[i] : D;
+  }
   float host_scale[3] = {1.f, 1.f, 1.f};
   float* dev_scale[3] = {nullptr, nullptr, nullptr};
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };
   for (int i = 0; i < 3; ++i) {
-    const uint64_t count = rows[i] * D;
+    const uint64_t count = rows[i] * cols[i];
     const size_t qb = al(target_precision == MFA_PRECISION_INT8 ? count : (count + 1) / 2);
     const uint64_t nb = mode == MFA_QUANT_BLOCKWISE
-                            ? ((rows[i] + block_size - 1) / block_size) * ((D + block_size - 1) / block_size)
+                            ? ((rows[i] + block_size - 1) / block_size) * ((cols[i] + block_size - 1) / block_size)
                             : 0;
-    const size_t ws = al(mfa_quantize_workspace_size(count, (uint32_t)rows[i], (uint32_t)D, mode, block_size));
+    const size_t ws = al(mfa_quantize_workspace_size(count, (uint32_t)rows[i], (uint32_t)cols[i], mode, block_size));
     const size_t bytes = qb + 256 + ws + 2 * al(nb * 4);
     void* buf = nullptr;
     if (mfa::plan_capture()) return fail(MFA_ERR_UNSUPPORTED, "plan query of the runtime-quantising forward");
@@ -968,7 +979,7 @@ extern "C" mfa_status_t mfa_quantized_forward_from_float(
     void* work = c + qb + 256;
     float* bsc = nb ? (float*)(c + qb + 256 + ws) : nullptr;
     int32_t* bzp = nb ? (int32_t*)(c + qb + 256 + ws + al(nb * 4)) : nullptr;
-    st = mfa_quantize(in[i], precs[i], count, (uint32_t)rows[i], (uint32_t)D, target_precision, mode,
+    st = mfa_quantize(in[i], precs[i], count, (uint32_t)rows[i], (uint32_t)cols[i], target_precision, mode,
                       block_size, c, dev_scale[i], bsc, bzp, ws ? work : nullptr, stream);
     if (st != MFA_SUCCESS) return st;
     t[i].data = c;
@@ -1061,7 +1072,7 @@ enum BwdPhase { PHASE_QUERY = 1, PHASE_KV = 2, PHASE_BOTH = 3 };
 // registers, takes per-tensor quantised K/V (INT8/INT4, dense rows) directly.
 bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int qsrc,
                        bool kv_quant = false) {
-  if (const char* e = getenv("MFA_DISABLE_FAST")) {
+  if (const char* e = mfa::dev_env("MFA_DISABLE_FAST")) {
     if (e[0] == '1') return false;
   }
   if (elem != 1 && elem != 2) return false;
@@ -1094,8 +1105,10 @@ bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int 
   return true;
 }
 
+// kv_widen: quantised K/V (16-bit Q) may run the tuned key-phase kernel, which widens them in
+// registers (quantized_backward decides it; false everywhere else).
 mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ksrc, int qsrc,
-                          int phase, hipStream_t stream) {
+                          int phase, hipStream_t stream, bool kv_widen = false) {
   mfa::BwdParams p = base_p;
   if (mfa_status_t st = check_keys(p.R, p.C)) return st;
   if (p.R == 0)
@@ -1121,13 +1134,13 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
   if (phase & PHASE_KV) {
     p.nblk = (p.C + bp - 1) / bp;
     if (p.C > 0) {
-      // Quantised K/V with 16-bit Q reach here only for backwardKeyValue alone (see
-      // quantized_backward): its fast kernel widens them in registers.
-      const bool fast_kv = fast || (!big && ksrc > 0 && bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true));
+      // Quantised K/V with 16-bit Q: the tuned kernel widens them in registers when
+      // quantized_backward chose that (kv_widen); otherwise the generic kernel dequantises.
+      const bool fast_kv = fast || (!big && ksrc > 0 && kv_widen);
       // D = 256 calls the tuned kernel does not take (strides, transposes): the generic kernel.
       // MFA_BWD256_BIGD=1 runs the D-blocked kernel in two 128-column slices instead (measured
       // 3x slower: each slice recomputes S and dP over all 256 columns on 32-row tiles).
-      const char* b256 = getenv("MFA_BWD256_BIGD");
+      const char* b256 = mfa::dev_env("MFA_BWD256_BIGD");
       const bool blocked = !big && !fast_kv && DP == 256 && elem != 0 && ksrc == 0 && qsrc == 0 &&
                            b256 && b256[0] == '1';
       hipError_t e = big || blocked ? mfa::bwd_bigd_dispatch(p, 1, elem, stream)
@@ -1295,10 +1308,12 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   // backwardKeyValue alone with 16-bit Q: its kernel reads each key block's K/V rows once per
   // workgroup into registers and widens them there, so the pass would only add traffic
   // (MFA_KV_REGS=0 keeps the pass: A/B, bit-identity tests).
-  const char* kvr = getenv("MFA_KV_REGS");
-  const bool kv_regs = phase == PHASE_KV && ksrc > 0 && qsrc == 0 && !(kvr && kvr[0] == '0') &&
-                       !dequant_pass_needed(D) &&
-                       bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true);
+  // Where no pass runs (small problems), the key phase widens in registers too, unless
+  // MFA_KV_REGS=0.
+  const char* kvr = mfa::dev_env("MFA_KV_REGS");
+  const bool kv_widen = ksrc > 0 && qsrc == 0 && !(kvr && kvr[0] == '0') &&
+                        !dequant_pass_needed(D) && bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true);
+  const bool kv_regs = phase == PHASE_KV && kv_widen;
   if (dequant_pass_worth(R, H, Hkv, D, elem) && !kv_regs) {
     hipStream_t s = (hipStream_t)stream;
     if (ksrc > 0) {
@@ -1311,7 +1326,7 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
       qsrc = 0;
     }
   }
-  return run_backward(p, elem, DP, ksrc, qsrc, phase, (hipStream_t)stream);
+  return run_backward(p, elem, DP, ksrc, qsrc, phase, (hipStream_t)stream, kv_widen);
 }
 
 }  // namespace

@@ -77,16 +77,10 @@ size_t fwd_stream_workspace_bytes(const FwdParams& p, int elem, int DP, size_t* 
 hipError_t fwd_stream_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
-// One wave per SIMD, two query sub-blocks per wave, O in kernel-owned AGPRs
-// (attention_fwd_aw.hip): D = 128, no mask or causal.
-hipError_t fwd_aw_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Dense 16-bit copy [B, Hx, S, D] of a quantised operand holding the MFMA operands the
 // dequantise-on-load staging would produce (kv_dequant.hip).
 hipError_t kv_dequant_dispatch(const Operand& op, int B, int Hx, int S, int D, int elem,
                                void* out, hipStream_t stream);
-// First-generation tuned 16-bit forward (attention_fwd_fast.hip): D = 64 / 128 16-bit K/V and
-// INT8 K/V at D = 128 dequantised on load; hipErrorNotSupported when the shape is not covered.
-hipError_t fwd_fast_dispatch(const FwdParams& p, int elem, int DP, int kvsrc, hipStream_t stream);
 // INT8 K/V on the integer matrix cores (attention_fwd_i8.hip); 128-query blocks.
 hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream);
 hipError_t gemm_dispatch(const GemmParams& p, int prec_ab, int batch, hipStream_t stream);

@@ -27,6 +27,18 @@
 
 namespace mfa {
 
+// Development A/B switches (MFA_FWD_SHARE, MFA_KV_REGS, MFA_GEMM3, ...) change which kernel a
+// call launches.  They are read only in a process started with MFA_DEV=1 (the test suite and
+// the A/B tools set it; read once, at the first dispatch), so a production caller's
+// environment can never change the plan, and the dispatch path calls no getenv otherwise.
+inline const char* dev_env(const char* name) {
+  static const bool dev = [] {
+    const char* e = std::getenv("MFA_DEV");
+    return e != nullptr && e[0] == '1' && e[1] == 0;
+  }();
+  return dev ? std::getenv(name) : nullptr;
+}
+
 struct LaunchRec {
   char name[96];
   uint32_t threads;

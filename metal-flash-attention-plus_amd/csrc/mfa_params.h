@@ -19,8 +19,10 @@ struct Operand {
   const int32_t* bzp;     // blockwise zero points (NULL: zero)
   int32_t bsize;          // block size (elements) of the 2-D [rows, cols] block grid
   int32_t bcols;          // ceil(cols / bsize)
-  int32_t cols;           // columns of the 2-D quantisation view (= head dim)
-  int32_t pad0;
+  int32_t cols;           // columns of the 2-D quantisation view: the head dim, or S when qtr
+  int32_t qtr;            // transposed quantised operand: the block grid is over the memory
+                          // view [D rows][S cols] per head (AttentionKernel+Accumulate.swift:
+                          // 461-472: row = d, col = seq, ceil(leadingDimension / BLOCK_SIZE_K))
 };
 
 struct MaskArgs {

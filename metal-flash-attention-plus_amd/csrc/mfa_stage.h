@@ -31,24 +31,30 @@ __device__ __forceinline__ int8_t ld_i4(const uint8_t* base, int64_t e) {
   return (int8_t)(nib - 8);
 }
 
-// Row of the 2-D [rows, cols] quantisation view holding row `row` of head (b, hx).  Quantised
-// operands are dense (row-major or transposed within each head, make_operand), so head (b, hx)
-// starts at view row (b·sb + hx·sh) / cols whatever the layout inside the head; the element
-// offset divided by cols would give the wrong row for a transposed head (ss = 1).
-__device__ __forceinline__ int64_t quant_row(const Operand& op, int b, int hx, int64_t row) {
-  return ((int64_t)b * op.sb + (int64_t)hx * op.sh) / op.cols + row;
+// First row of head (b, hx) in the 2-D [rows, cols] quantisation view of a quantised operand.
+// Quantised operands are dense (row-major or transposed within each head, make_operand), so the
+// head starts at view row (b·sb + hx·sh) / cols whatever the layout inside the head.  The view
+// is the operand's memory layout, as the reference's factory quantises a buffer
+// (GEMMQuantization.swift:561-575): row-major [S][D] rows (cols = D), or, for a transposed
+// operand, [D][S] rows (cols = S; AttentionKernel+Accumulate.swift:461-472 and
+// AttentionKernel+OuterProduct.swift:301-316 index it with row = d, col = seq).
+__device__ __forceinline__ int64_t quant_row(const Operand& op, int b, int hx) {
+  return ((int64_t)b * op.sb + (int64_t)hx * op.sh) / op.cols;
 }
 
-// Dequantised value of quantised element (row2d, col) with integer payload qv.
-__device__ __forceinline__ float dequant(const Operand& op, int qv, int64_t row2d, int col) {
+// Dequantised value of quantised element (sequence row `row`, column `col`) of the head whose
+// first view row is `hrow`, with integer payload qv.
+__device__ __forceinline__ float dequant(const Operand& op, int qv, int64_t hrow, int64_t row,
+                                         int col) {
   if (op.bscale) {
-    const int64_t bi = (row2d / op.bsize) * op.bcols + col / op.bsize;
+    const int64_t vr = op.qtr ? hrow + col : hrow + row;
+    const int64_t vc = op.qtr ? row : col;
+    const int64_t bi = (vr / op.bsize) * op.bcols + vc / op.bsize;
     const int zp = op.bzp ? op.bzp[bi] : 0;
     return (float)(qv - zp) * op.bscale[bi];
   }
   return (float)(qv - op.zp);  // per-tensor scale folded by the host
 }
-
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
@@ -136,10 +142,11 @@ __device__ __forceinline__ uint4 load_qchunk(const Operand& op, int64_t rowoff, 
 
 // The MFMA-type chunk of a quantised chunk: per-tensor the exact integers q - zp (the scale is
 // folded by the host); blockwise the dequantised value (q - zp)·s rounded to the element type.
-// `row2d` is the row of the [rows, cols] quantisation view; invalid rows give zeros.
+// `hrow` is the head's first view row (quant_row), `row` the sequence row; invalid rows give
+// zeros.
 template <class E, int SRC>
-__device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& op, int64_t row2d,
-                                                int d0, int D, bool valid) {
+__device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& op, int64_t hrow,
+                                                int64_t row, int d0, int D, bool valid) {
   if (!op.bscale) return dequant_fast<E, SRC>(raw, (float)op.zp);
   uint32_t w[4];
 #pragma unroll
@@ -156,7 +163,7 @@ __device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& 
         qv = (int)((raw.x >> (4 * j)) & 15u) - 8;
       }
       float x = 0.f;
-      if (valid && d0 + j < D) x = dequant(op, qv, row2d, d0 + j);
+      if (valid && d0 + j < D) x = dequant(op, qv, hrow, row, d0 + j);
       packed |= (uint32_t)E::from_f32(x) << (16 * e);
     }
     w[jj] = packed;
@@ -277,8 +284,8 @@ struct Stager {
           // Per-tensor: the exact integers (q - zp); zero-filled loads beyond the tile edge
           // only ever meet zero Q columns or masked keys.
           const int grow = row0 + r;
-          const int64_t row2d = op.bscale ? quant_row(op, b, hx, grow) : 0;
-          out = convert_qchunk<typename A::Elem, SRC>(raw[i], op, row2d, c * 8, D, grow < nrows);
+          const int64_t hrow = op.bscale ? quant_row(op, b, hx) : 0;
+          out = convert_qchunk<typename A::Elem, SRC>(raw[i], op, hrow, grow, c * 8, D, grow < nrows);
         }
         *reinterpret_cast<uint4*>(tile + A::TileT::off(r, c)) = out;
       }
@@ -301,7 +308,7 @@ __device__ __forceinline__ void load_row_frags(typename A::frag (&f)[A::DSTEPS],
       f[s] = (valid && d < D) ? base[(int64_t)d * op.sd] : 0.f;
     }
   } else {
-    const int64_t row2d = (op.prec == P_INT8 || op.prec == P_INT4) ? quant_row(op, b, hx, row) : 0;
+    const int64_t hrow = (op.prec == P_INT8 || op.prec == P_INT4) ? quant_row(op, b, hx) : 0;
 #pragma unroll
     for (int s = 0; s < A::DSTEPS; ++s) {
       const int d0 = 16 * s + 8 * h;
@@ -314,7 +321,7 @@ __device__ __forceinline__ void load_row_frags(typename A::frag (&f)[A::DSTEPS],
             const int64_t e = rowoff + (int64_t)(d0 + j) * op.sd;
             const int qv = op.prec == P_INT8 ? (int)((const int8_t*)op.ptr)[e]
                                              : (int)ld_i4((const uint8_t*)op.ptr, e);
-            x = dequant(op, qv, row2d, d0 + j);
+            x = dequant(op, qv, hrow, row, d0 + j);
           }
           v[j] = (short)A::Elem::from_f32(x);
         }

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# The tests A/B the library's development switches (MFA_FWD_SHARE, MFA_KV_REGS, ...), which the
+# library reads only in a process started with MFA_DEV=1 (mfa_launch.h dev_env): set it before
+# the library is loaded.  tests/test_dev_gate.py checks a process without it.
+os.environ.setdefault("MFA_DEV", "1")
+
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(_REPO, "tests"))
 sys.path.insert(0, os.path.join(_REPO, "metal-flash-attention-plus_amd", "python"))

@@ -141,3 +141,48 @@ def test_stream_large_causal_heads(gpu, prec):
         ref_l = (m.squeeze(1) + torch.log(p.sum(dim=1))) / np.log(2)
         assert (o[bb, hh].double() - ref_o).abs().max().item() <= (5e-3 if prec == FP16 else 1e-2)
         assert (l[bb, hh].double() - ref_l).abs().max().item() <= 7e-3 + 4e-3
+
+
+def _torch_ref_check(q, k, v, o, l, slices, tol_o):
+    D = q.shape[-1]
+    for bb, hh in slices:
+        Qd, Kd, Vd = (t[bb, hh].double() for t in (q, k, v))
+        s = (Qd @ Kd.T) / np.sqrt(D)
+        s = s + torch.triu(torch.full_like(s, float("-inf")), diagonal=1)
+        m = s.max(dim=1, keepdim=True).values
+        p = torch.exp(s - m)
+        ref_o = (p @ Vd) / p.sum(dim=1, keepdim=True)
+        ref_l = (m.squeeze(1) + torch.log(p.sum(dim=1))) / np.log(2)
+        assert (o[bb, hh].double() - ref_o).abs().max().item() <= tol_o
+        assert (l[bb, hh].double() - ref_l).abs().max().item() <= 7e-3 + 4e-3
+
+
+def test_stream_workspace_counter_region_grows(gpu):
+    # the stream kernel's arrival counters sit at the front of the library
+    # workspace and its partial states right behind them.  A second call on the same stream
+    # whose counter region is longer than the first's (D128 B4 -> D64 B8 at H16 S4096) must not
+    # read the first call's partial states as counters: both results against a float64
+    # restatement, and the second call repeated bit for bit.
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    outs = []
+    for B, D in ((4, 128), (8, 64)):
+        H, S = 16, 4096
+        q, k, v = ((torch.rand((B, H, S, D), generator=g, device="cuda:0") * 2 - 1).half()
+                   for _ in range(3))
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=FP16, causal=True)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+        o = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device="cuda:0")
+        l = torch.full((B, H, S), float("nan"), dtype=torch.float16, device="cuda:0")
+        mfa.last_launches()
+        mfa.MultiHeadAttention().forward(desc, q, k, v, o, l)
+        torch.cuda.synchronize()
+        assert launched()[-1].startswith("mfa_fwd2_stream_kernel"), launched()
+        assert not torch.isnan(o).any() and not torch.isnan(l).any()
+        _torch_ref_check(q, k, v, o, l, ((0, 0), (B // 2, 7), (B - 1, 15)), 5e-3)
+        outs.append((desc, q, k, v, o.clone(), l.clone()))
+    desc, q, k, v, o1, l1 = outs[1]
+    o = torch.empty_like(o1)
+    l = torch.empty_like(l1)
+    mfa.MultiHeadAttention().forward(desc, q, k, v, o, l)
+    torch.cuda.synchronize()
+    assert torch.equal(o, o1) and torch.equal(l, l1)

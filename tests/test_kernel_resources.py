@@ -23,18 +23,19 @@ HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd2_share_kernel", "mfa_
        "mfa_bwd_q_fast_kernel", "mfa_bwd_kv_fast_kernel", "mfa_fwd_bigd_kernel",
        "mfa_bwd_q_bigd_kernel", "mfa_mla", "mfa_kv_dequant_kernel", "mfa_gemm2_kernel",
        "mfa_gemm3_kernel", "qz_")
-# Known stack users, each a rare path: the D > 256 backwardQuery with an FP32 dO (the quantised
-# API's dO, DOS = SRC_F32ANY) keeps 160 B of its 64-register dO staging in scratch (no spill:
-# vgpr_spill_count 0).
-# The D = 256 backwardKeyValue mask instantiation (additive masks / sparse ranges; the
-# unmasked D = 256 kernel sits exactly at 512 registers) spills ~40 registers: it issues the next
-# step's tiles after its S/dP chains so the reloads never wait on them, and runs the masked
-# D = 256 backwardKeyValue 5.7x faster than the generic kernel it replaced (257 vs 1464 us,
-# B1 H16 S2048 additive mask).
-EXEMPT = ("mfa_bwd_q_bigd_kernelINS_7Arith16INS_3F16ELi128EEELi128ELi3E",
-          "mfa_bwd_q_bigd_kernelINS_7Arith16INS_4BF16ELi128EEELi128ELi3E",
-          "mfa_bwd_kv_fast_kernelINS_3F16ELi256ELi32ELi0ELb1E",
-          "mfa_bwd_kv_fast_kernelINS_4BF16ELi256ELi32ELi0ELb1E")
+# Known stack users, each a rare path, with a cap on what they may use (bytes of scratch per
+# lane, spilled VGPRs) so that growth is caught:
+# - the D > 256 backwardQuery with an FP32 dO (the quantised API's dO, DOS = SRC_F32ANY) keeps
+#   160 B of its 64-register dO staging in scratch (no spill: vgpr_spill_count 0);
+# - the D = 256 backwardKeyValue mask instantiation (additive masks / sparse ranges; the unmasked
+#   D = 256 kernel sits exactly at 512 registers) spills 24 registers (52 B): it issues the next
+#   step's tiles after its S/dP chains so the reloads never wait on them, and runs the masked
+#   D = 256 backwardKeyValue 5.7x faster than the generic kernel it replaced (257 vs 1464 us,
+#   B1 H16 S2048 additive mask).
+EXEMPT = {"mfa_bwd_q_bigd_kernelINS_7Arith16INS_3F16ELi128EEELi128ELi3E": (160, 0),
+          "mfa_bwd_q_bigd_kernelINS_7Arith16INS_4BF16ELi128EEELi128ELi3E": (160, 0),
+          "mfa_bwd_kv_fast_kernelINS_3F16ELi256ELi32ELi0ELb1E": (64, 32),
+          "mfa_bwd_kv_fast_kernelINS_4BF16ELi256ELi32ELi0ELb1E": (64, 32)}
 
 
 @pytest.fixture(scope="module")
@@ -72,6 +73,14 @@ def test_hot_kernels_use_no_scratch(kernels):
     bad = {n: k for n, k in kernels.items()
            if any(f in n for f in HOT) and k["scratch"] != 0 and not any(e in n for e in EXEMPT)}
     assert not bad, bad
+
+
+def test_exempt_kernels_stay_within_caps(kernels):
+    for frag, (max_scratch, max_spill) in EXEMPT.items():
+        hits = {n: k for n, k in kernels.items() if frag in n}
+        assert hits, frag
+        for n, k in hits.items():
+            assert k["scratch"] <= max_scratch and k["vgpr_spill"] <= max_spill, (n, k)
 
 
 def test_hot_kernels_fit_register_file(kernels):

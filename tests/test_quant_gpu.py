@@ -662,63 +662,113 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, monkeypatch):
         assert maxerr(o1, o2) < 1e-5 and maxerr(l1, l2) < 2e-2
 
 
+def _ref_dequant_transposed_block(e, B, H, S, D, bs, scales):
+    """The reference's block lookup for a transposed quantised operand, written out per element
+    (AttentionKernel+Accumulate.swift:461-472, AttentionKernel+OuterProduct.swift:301-316):
+    the head's memory is [D][S]; element (seq c, dim d) of head (b, h) uses block
+    ((row0 + d) / bs) * ceil(S / bs) + c / bs with row0 = (b * H + h) * D, because rowExpr =
+    d_outer + d, colExpr = traversal + c and num_blocks_col = ceil(leadingDimension / bs),
+    leadingDimension = S when transposed.  `e` holds the integers in memory order [B, H, D, S]
+    (INT8 as stored; INT4 as q - 8 already).  Returns the logical [B, H, S, D] values."""
+    nbc = (S + bs - 1) // bs
+    out = np.empty((B, H, S, D), np.float32)
+    c = np.arange(S)[:, None]
+    d = np.arange(D)[None, :]
+    for b in range(B):
+        for h in range(H):
+            row0 = (b * H + h) * D
+            bi = ((row0 + d) // bs) * nbc + c // bs           # [S, D]
+            out[b, h] = e[b, h].T.astype(np.float32) * scales[bi]
+    return out
+
+
 @pytest.mark.parametrize("blockwise", [None, 16])
 @pytest.mark.parametrize("kv", [P.INT8, P.INT4])
-def test_transposed_quantized_kv_matches_row_major(gpu, blockwise, kv):
+def test_transposed_quantized_kv_matches_reference_layout(gpu, blockwise, kv):
     # A transposed K / V (column-major within each head, AttentionKernelDescriptor
-    # transposeState) changes where the bytes sit, not which block scale an element uses: the
-    # blockwise view is the logical [B·Hkv·S, D] one (the scale row was taken from
-    # the element offset, which reads row 0's scales for every row s < D of a transposed head).
-    # Same quantised values and scales in both layouts: both outputs match attention on the
-    # dequantised values (the two layouts may run different kernels, so not bit for bit).
+    # transposeState).  Blockwise scales follow the reference's lookup for transposed operands:
+    # the block grid is over the memory view [B·H·D rows][S cols] (ADVICE r4: it was the
+    # logical [B·H·S, D] grid).  The quantised tensor is made as the reference's factory makes
+    # it for that buffer: its memory view quantised block by block.  Expected values come from
+    # the reference's index formula written out per element (_ref_dequant_transposed_block),
+    # not from the repo's quantiser; the row-major run checks against its own view.
     B, H, S, D = 1, 2, 96, 64
     rng = np.random.default_rng(21)
     Q, K, V = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
-    # Column scale ramps make a wrong scale row visible.
+    # Column and row scale ramps make a wrong block lookup visible.
     K *= np.linspace(0.2, 3.0, S, dtype=np.float32)[None, None, :, None]
     V *= np.linspace(3.0, 0.2, S, dtype=np.float32)[None, None, :, None]
+    K *= np.linspace(0.5, 2.0, D, dtype=np.float32)[None, None, None, :]
     tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
-    keep, deq = [], []
+    keep = []
 
     def qt(x, transposed):
-        rows, cols = x.size // D, D
+        mem = np.ascontiguousarray(x.transpose(0, 1, 3, 2)) if transposed else x
+        rows, cols = (B * H * D, S) if transposed else (B * H * S, D)
         if blockwise:
-            sc = ol.quant_scales_block(x, rows, cols, blockwise, int(kv))
-            q = ol.quantize_block(x, cols, blockwise, int(kv), sc)
+            sc = ol.quant_scales_block(mem, rows, cols, blockwise, int(kv))
+            q = ol.quantize_block(mem, cols, blockwise, int(kv), sc)
             kw = {"block_scales": tdev(sc), "block_size": blockwise}
-            if not transposed:
-                deq.append(ol.dequantize_block(q, x.size, cols, blockwise, int(kv), sc).reshape(x.shape))
         else:
-            s = ol.quant_scale_tensor(x, int(kv))
-            q = ol.quantize(x, int(kv), s)
+            s = ol.quant_scale_tensor(mem, int(kv))
+            q = ol.quantize(mem, int(kv), s)
             kw = {"scale": s}
-            if not transposed:
-                deq.append(ol.dequantize(q, x.size, int(kv), s).reshape(x.shape))
-        if kv == P.INT4:  # unpack nibbles (element 2i low) to permute them, then repack
-            e = np.empty(x.size, np.uint8)
-            e[0::2], e[1::2] = q[: (x.size + 1) // 2] & 15, q[: x.size // 2] >> 4
-        else:
-            e = np.asarray(q, np.uint8)[: x.size]
-        if transposed:
-            e = np.ascontiguousarray(e.reshape(B, H, S, D).transpose(0, 1, 3, 2)).ravel()
         if kv == P.INT4:
-            e = (e[0::2] | (e[1::2] << 4)).astype(np.uint8)
-        t = mfa.quantized_tensor(tdev(e, torch.uint8), kv, **kw)
+            ints = np.empty(x.size, np.int32)
+            ints[0::2], ints[1::2] = (q[: (x.size + 1) // 2] & 15), (q[: x.size // 2] >> 4)
+            ints -= 8
+        else:
+            ints = np.asarray(q[: x.size]).view(np.int8).astype(np.int32)
+        if transposed and blockwise:
+            deq = _ref_dequant_transposed_block(ints.reshape(B, H, D, S), B, H, S, D, blockwise, sc)
+        elif blockwise:
+            deq = ol.dequantize_block(q, x.size, cols, blockwise, int(kv), sc).reshape(x.shape)
+        else:
+            deq = (ints.astype(np.float32) * np.float32(s)).reshape(mem.shape)
+            if transposed:
+                deq = np.ascontiguousarray(deq.transpose(0, 1, 3, 2))
+        t = mfa.quantized_tensor(tdev(q, torch.uint8), kv, **kw)
         keep.append(t)
-        return t
+        return t, deq
 
-    outs = []
     for tr in (False, True):
         base = mfa.AttentionDescriptor.make(S, S, D, transpose=(False, tr, tr, False))
         desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H, Hkv=H)
         o = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
-        mfa.QuantizedAttention().forward(desc, tq, qt(K, tr), qt(V, tr), o)
+        (tk, dk), (tv, dv) = qt(K, tr), qt(V, tr)
+        mfa.QuantizedAttention().forward(desc, tq, tk, tv, o)
         torch.cuda.synchronize()
-        outs.append(o)
-    ref = ol.attention(seen(Q, P.FP16), deq[0], deq[1])["O"]
-    for o in outs:
+        ref = ol.attention(seen(Q, P.FP16), dk, dv)["O"]
         assert torch.isfinite(o).all()
-        assert maxerr(o, ref) < 5e-3
+        assert maxerr(o, ref) < 5e-3, tr
+
+
+def test_forward_from_float_transposed_blockwise(gpu):
+    # The runtime-quantising entry quantises a transposed buffer as its memory view, so the
+    # result equals quantising that view by hand and calling mfa_quantized_forward.
+    B, H, S, D, bs = 1, 2, 128, 64, 32
+    rng = np.random.default_rng(5)
+    Q, K, V = (rng.standard_normal((B, H, S, D)).astype(np.float32) for _ in range(3))
+    K *= np.linspace(0.2, 3.0, S, dtype=np.float32)[None, None, :, None]
+    Kt, Vt = (np.ascontiguousarray(x.transpose(0, 1, 3, 2)) for x in (K, V))
+    base = mfa.AttentionDescriptor.make(S, S, D, transpose=(False, True, True, False))
+    desc = mfa.quantized_descriptor(base, P.INT8, P.INT8, P.INT8, B=B, H=H, Hkv=H)
+    o1 = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
+    mfa.QuantizedAttention().forward_from_buffers(desc, tdev(Q), tdev(Kt), tdev(Vt), o1, P.INT8,
+                                                  mfa.QuantMode.blockwise, bs)
+    torch.cuda.synchronize()
+    keep = []
+    ts = []
+    for x, rows, cols in ((Q, B * H * S, D), (Kt, B * H * D, S), (Vt, B * H * D, S)):
+        sc = ol.quant_scales_block(x, rows, cols, bs, int(P.INT8))
+        q = ol.quantize_block(x, cols, bs, int(P.INT8), sc)
+        t = mfa.quantized_tensor(tdev(q, torch.uint8), P.INT8, block_scales=tdev(sc), block_size=bs)
+        keep.append(t)
+        ts.append(t)
+    o2 = torch.full_like(o1, float("nan"))
+    mfa.QuantizedAttention().forward(desc, *ts, o2)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
 
 
 @pytest.mark.parametrize("target,mode,bs", [(P.INT8, mfa.QuantMode.tensorWise, 0),

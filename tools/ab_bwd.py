@@ -6,6 +6,7 @@ Usage: python tools/ab_bwd.py VAR=a,b [--shape B,H,S,D] [--rounds N]"""
 import argparse
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import statistics
 import sys
 

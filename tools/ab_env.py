@@ -8,6 +8,7 @@ unsets the variable (the library default).
 """
 import itertools
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import statistics
 import sys
 

@@ -4,6 +4,7 @@
 import argparse
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import statistics
 import sys
 

@@ -5,6 +5,7 @@ Usage: python tools/ab_gemm.py VAR=a,b [--mnk M,N,K] [--bf16]"""
 import argparse
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import statistics
 import sys
 

@@ -5,6 +5,7 @@ Usage: python tools/ab_mla.py VAR=a,b [--rounds N]"""
 import argparse
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import statistics
 import sys
 

@@ -6,6 +6,7 @@ per-shape TFLOP/s.  Usage: python tools/causal_probe.py
 """
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import sys
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

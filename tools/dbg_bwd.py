@@ -1,5 +1,6 @@
 """Debug: fast vs generic backward error table (development tool)."""
 import os, sys
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 import numpy as np
 import conftest  # noqa: F401  (sys.path setup)

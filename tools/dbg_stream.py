@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Debug: stream-split causal forward vs the mirrored kernel, error per 128-row group."""
 import os, sys
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(_REPO, "metal-flash-attention-plus_amd", "python"))
 import numpy as np

@@ -1,5 +1,6 @@
 """Development: interleaved A/B of MFA_GEMM_IMG on 4096^3 fp16 NN/NT/TN and the C4 decompress shape."""
 import os, sys, torch
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 sys.path.insert(0, 'metal-flash-attention-plus_amd/python')
 import mfa_amd as mfa
 P = mfa.Precision

@@ -7,6 +7,7 @@ a = (torch.rand((n, n), device='cuda') - 0.5).half()
 b = (torch.rand((n, n), device='cuda') - 0.5).half()
 c = torch.empty((n, n), device='cuda', dtype=torch.float16)
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 for ta, tb, nn in ((0, 0, '0'), (0, 0, '3'), (0, 1, '0'), (1, 0, '0'), (0, 0, '0'), (0, 0, '3')):
     os.environ['MFA_GEMM_NN'] = nn
     f = lambda: mfa.gemm(a, b, c, n, n, n, P.FP16, P.FP16, transpose_a=bool(ta), transpose_b=bool(tb))

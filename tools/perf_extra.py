@@ -3,6 +3,7 @@
 (transposed / mixed-precision GEMMDescriptor cases) and the Hadamard rotation."""
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import sys
 
 import torch

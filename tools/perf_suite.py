@@ -13,6 +13,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import sys
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -2,6 +2,7 @@
 """Runs one hot-path configuration a few times (a short program for rocprofv3 PMC passes).
 Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv,mla_dec,quant} [reps]"""
 import os
+os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import sys
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
