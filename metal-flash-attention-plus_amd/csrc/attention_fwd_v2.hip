@@ -945,6 +945,13 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
                    (sv ? sv[0] == '1'
                        : (p.nblk % 2 == 0 || p.nblk >= 8) &&
                              (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);
+  if (adj && elem == P_FP16 && DP == 128) {
+    const char* pp = mfa::dev_env("MFA_FWD_PIPE");
+    if (pp && pp[0] == '1') {
+      const hipError_t e = fwd_pipe_dispatch(p, elem, DP, stream);
+      if (e != hipErrorNotSupported) return e;
+    }
+  }
 #define MFA_F2(ELEM, EE, DPV, BKV, WPS)                                          \
   if (elem == ELEM && DP == DPV && adj)                                         \
     return launch_fwd2_share<EE, DPV, BKV, false>(p, stream);                   \

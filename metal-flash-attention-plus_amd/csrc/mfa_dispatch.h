@@ -75,6 +75,9 @@ hipError_t fwd_kv8_dispatch(const FwdParams& p, int elem, int src, hipStream_t s
 // and the launch (p.ws set).
 size_t fwd_stream_workspace_bytes(const FwdParams& p, int elem, int DP, size_t* zero_bytes);
 hipError_t fwd_stream_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
+// Software-pipelined fp16 D = 128 forward (attention_fwd_pipe.hip); hipErrorNotSupported when
+// the shape or mask is not covered.
+hipError_t fwd_pipe_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Second-generation 16-bit forward (attention_fwd_v2.hip).
 hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t stream);
 // Dense 16-bit copy [B, Hx, S, D] of a quantised operand holding the MFMA operands the
