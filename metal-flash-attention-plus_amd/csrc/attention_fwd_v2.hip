@@ -945,9 +945,12 @@ hipError_t fwd2_dispatch(const FwdParams& p, int elem, int DP, hipStream_t strea
                    (sv ? sv[0] == '1'
                        : (p.nblk % 2 == 0 || p.nblk >= 8) &&
                              (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256);
+  // Adjacent fp16 D = 128 pairs: the software-pipelined kernel with hand-placed blocks
+  // (attention_fwd_pipe.hip; bit-identical, +1.1 % at C3 in one-process A/B).  MFA_FWD_PIPE=0
+  // keeps the compiler-scheduled shared-tile kernel (A/B).
   if (adj && elem == P_FP16 && DP == 128) {
     const char* pp = mfa::dev_env("MFA_FWD_PIPE");
-    if (pp && pp[0] == '1') {
+    if (!(pp && pp[0] == '0')) {
       const hipError_t e = fwd_pipe_dispatch(p, elem, DP, stream);
       if (e != hipErrorNotSupported) return e;
     }

@@ -95,19 +95,26 @@ def test_pipe_rescale_every_tile(gpu):
     check_pipe(Q, K, V, tol_o=5e-3, tol_l=2e-2)
 
 
-def test_pipe_matches_shared_tile_kernel(gpu):
-    # C3's shape class at a smaller head count: the same schedule of staged tiles and the same
-    # arithmetic per element; the sums run in the same order, so O and L agree to rounding.
+@pytest.mark.parametrize("spike_key", [None, 0, 1000])
+def test_pipe_matches_shared_tile_kernel(gpu, spike_key):
+    # The same staged tiles, the same arithmetic per element and the row sums in the same order
+    # (fwd2_exp's, split across the two blocks): bit-identical O and L to the compiler-scheduled
+    # shared-tile kernel, also when a rescale recomputes the speculative exponentials.
     B, H, S, D = 1, 4, 2048, 128
     Q, K, V = (gaussian((B, H, S, D), 50 + i) for i in range(3))
+    if spike_key is not None:
+        direction = np.ones(D, dtype=np.float32) / np.sqrt(D)
+        Q += 2.0 * direction
+        K[:, :, spike_key] = 20.0 * direction
     with env(**PIPE):
         mfa.last_launches()
         o1, l1 = run_forward(Q, K, V, prec=FP16)
         assert launched()[-1].startswith("mfa_fwd_pipe_kernel")
-    with env(MFA_FWD_SHARE=1):
+    with env(MFA_FWD_SHARE=1, MFA_FWD_PIPE=0):
+        mfa.last_launches()
         o0, l0 = run_forward(Q, K, V, prec=FP16)
-    assert maxerr(o1, o0) <= 1e-5
-    assert maxerr(l1.float(), l0.float()) <= 1e-5
+        assert launched()[-1].startswith("mfa_fwd2_share_kernel")
+    assert torch.equal(o1, o0) and torch.equal(l1, l0)
 
 
 def test_pipe_c3_heads(gpu):

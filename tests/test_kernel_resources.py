@@ -15,14 +15,15 @@ _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _LIB = os.path.join(_REPO, "metal-flash-attention-plus_amd", "libmfa_amd.so")
 _LLVM = "/opt/rocm/lib/llvm/bin"
 
-# Mangled-name fragments of the tuned kernels (csrc/attention_fwd_v2.hip, attention_fwd_stream.hip,
+# Mangled-name fragments of the tuned kernels (csrc/attention_fwd_v2.hip, attention_fwd_pipe.hip,
+# attention_fwd_stream.hip,
 # attention_fwd_i8.hip, attention_fwd_kv8.hip, attention_decode.hip, attention_bwd_fast.hip,
 # attention_bigd.hip, attention_mla_latent.hip, kv_dequant.hip, gemm.hip, quantize.hip).
 HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd2_share_kernel", "mfa_fwd2_stream_kernel",
        "mfa_fwd_i8_kernel", "mfa_fwd2_kv8_kernel", "mfa_fwd_decode_kernel", "mfa_decode_merge",
        "mfa_bwd_q_fast_kernel", "mfa_bwd_kv_fast_kernel", "mfa_fwd_bigd_kernel",
        "mfa_bwd_q_bigd_kernel", "mfa_mla", "mfa_kv_dequant_kernel", "mfa_gemm2_kernel",
-       "mfa_gemm3_kernel", "qz_")
+       "mfa_gemm3_kernel", "qz_", "mfa_fwd_pipe_kernel")
 # Known stack users, each a rare path, with a cap on what they may use (bytes of scratch per
 # lane, spilled VGPRs) so that growth is caught:
 # - the D > 256 backwardQuery with an FP32 dO (the quantised API's dO, DOS = SRC_F32ANY) keeps

@@ -44,7 +44,7 @@ def test_large_causal_runs_stream_split_kernel():
 def test_c3_runs_adjacent_shared_tile_kernel():
     # Unmasked with >= 256 block pairs: adjacent 128-row blocks share every K/V tile.
     p = one(mfa.multihead_plan(mh(1, 16, 8192, 128)))
-    assert p["name"] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>"
+    assert p["name"] == "mfa_fwd_pipe_kernel"
     assert p["threads"] == 512 and p["workgroups"] == 32 * 16
 
 
@@ -116,7 +116,7 @@ def test_quantized_plans():
     q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(q4)]
     assert names[:3] == ["mfa_kv_dequant_kernel<F16, 2>"] * 2 + ["mfa_kv_dequant_kernel<F16, 1>"]
-    assert names[3] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>"
+    assert names[3] == "mfa_fwd_pipe_kernel"
     # A non-zero zero point leaves the integer-matmul kernel (dequant-exact path instead).
     zp = mfa.QuantizedTensor(None, int(P.INT8), 0.5, 3)
     assert mfa.quantized_plan(qi, K.forward, None, zp, zp)[-1]["name"].startswith("mfa_fwd2_kv8_kernel<")
@@ -134,7 +134,7 @@ def test_kv8_override_takes_the_dequant_pass(monkeypatch):
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(qx)]
     assert names[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2
-    assert names[2] == "mfa_fwd2_share_kernel<F16, 128, 64, false, true, true, false>" and len(names) == 3
+    assert names[2] == "mfa_fwd_pipe_kernel" and len(names) == 3
 
 
 def test_environment_override_is_visible_in_plan(monkeypatch):

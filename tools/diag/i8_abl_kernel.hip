@@ -1,0 +1,378 @@
+// i8_abl_kernel.hip — DIAGNOSTIC COPY of attention_fwd_i8.hip (round 5) with timing ablations
+// (template ABL); not part of libmfa_amd.so.  The product kernel is the file in csrc/, whose
+// code this copy leaves untouched (an ablation parameter there changed its schedule).
+// Original header:
+// attention_fwd_i8.hip — INT8 K/V forward on the gfx950 integer matrix cores
+// (v_mfma_i32_32x32x32_i8, twice the fp16 MFMA rate).
+//
+// The reference runs quantised attention by dequantising K/V to FP32 on load and multiplying in
+// FP32 (GEMMHeaders.swift:679-738, QuantizedAttention.swift:135-263); the dequant-exact variant of
+// that lives in attention_fwd(_fast).hip.  This is the integer-MFMA variant the north star asks
+// for, with its own stated tolerance (the reference's INT8 gate, relative L2 error < 0.25 vs
+// the float reference, QuantizedAttentionTest.swift:519-520; measured error is reported by the
+// tests):
+//   * Q is quantised per row to INT8 in registers at kernel start (s_q = max|Q_row| / 127,
+//     round half away from zero, as GEMMQuantization.swift quantises);
+//   * S_int = Q_i8 · K_i8^T is exact in INT32; S = s_q · s_k · S_int;
+//   * softmax in FP32 as in the forward kernel, with the running max raised (to an integer)
+//     whenever it grows, so 0 <= P <= 1; then P' = round(127 · P) as INT8;
+//   * O_int += P' · V_i8 exact in INT32 (rescaled by an exact power of two when m moves);
+//     O = O_int · s_v / l', l' = Σ 127·P in FP32.
+// Layout: K and V tiles [key][d] int8 in LDS (XOR-swizzled 16-byte chunks).  K is read by rows;
+// V through ds_read_b64_tr_b8, whose lanes pick the keys in the order of the S accumulator
+// registers, so P'^T feeds O^T += V^T·P'^T straight from registers.
+#include "../../metal-flash-attention-plus_amd/csrc/attention_fwd2.h"
+
+namespace mfa {
+namespace diag {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float xh_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                                  __builtin_bit_cast(unsigned, x), false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ __forceinline__ float xh_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                                  __builtin_bit_cast(unsigned, x), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+// NG = 2 (unmasked forwards): a 512-thread workgroup of two 4-wave groups owns the adjacent
+// 128-row blocks (2·pi, 2·pi + 1), and every K/V tile, staged by all 8 waves, serves both
+// (256 query rows per staged tile, half the LDS-DMA of two 4-wave workgroups).
+// ABL (diagnostic builds only, tools/diag/i8_abl.hip; the library instantiates 0): timing
+// ablations — 1 no LDS-DMA in the loop, 2 no vmcnt wait / barrier in the loop, 4 no softmax
+// VALU (int->float, masks, max, rescale, exp2, row sum, byte pack), 8 no LDS fragment reads
+// (K / V fragments read once before the loop).  Wrong results for any code but 0.
+template <class E, int DP, int BK, int OCC, int NG, int ABL>
+__device__ __forceinline__ void mfa_fwd_i8_body(const FwdParams& p) {
+  static_assert(DP == 128 && (BK == 64 || BK == 128), "int8 kernel: D<=128, 64/128-key tiles");
+  using TK = Tile16<DP / 2>;            // [BK][DP bytes] = 16-byte chunks, DP/16 per row
+  constexpr int NT = 256 * NG, BQ = 128;
+  constexpr int NJ = BK / 32;
+  constexpr int KSTEPS = DP / 32;       // i8 MFMA k = 32
+  constexpr int KTILE = BK * DP;        // bytes
+  constexpr int VTILE = BK * DP;        // bytes
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const kb0 = smem;
+  char* const vb0 = smem + 2 * KTILE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = (tid & 255) >> 6;
+  const int grp = NG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int BH = p.B * p.H;
+  const int bid = blockIdx.x;
+  const int rb = NG > 1 ? NG * (bid / BH) + grp : p.nblk - 1 - bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
+  const int q0 = rb * BQ;
+  const int qi = q0 + wave * 32 + l32;
+  const bool qvalid = qi < p.R;
+
+  // ---- Q: load 64 of the row's 128 values (d = 32s + 16h + j), quantise per row.
+  i32x4 qf[KSTEPS];
+  float cq;
+  {
+    const uint16_t* qrow = (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh +
+                           (int64_t)(qvalid ? qi : 0) * p.q.ss;
+    float qv[KSTEPS][16];
+    float amax = 0.f;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      const int d0 = 32 * s + 16 * hh;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        i16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (qvalid && d0 + 8 * half < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0 + 8 * half);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = E::to_f32((uint16_t)v[j]);
+          qv[s][8 * half + j] = x;
+          amax = fmaxf(amax, fabsf(x));
+        }
+      }
+    }
+    amax = xh_max(amax);
+    const float sq = amax > 0.f ? amax / 127.0f : 1.0f;
+    const float rq = amax > 0.f ? 127.0f / amax : 1.0f;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      int w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // |x * rq| <= 127 (+ rounding), so the clamp only guards the last ulp.
+          const int qq = max(-127, min(127, (int)rintf(qv[s][4 * k + e] * rq)));
+          word |= ((uint32_t)qq & 0xffu) << (8 * e);
+        }
+        w[k] = (int)word;
+      }
+      qf[s] = i32x4{w[0], w[1], w[2], w[3]};
+    }
+    cq = p.c_log2 * sq;  // c_log2 already carries s_k
+  }
+
+  int kend = p.C;
+  if (p.mask.causal && p.mask.skip_ok) kend = min(kend, q0 + BQ);
+  int kbeg = 0;
+  if (p.mask.window && p.mask.skip_ok) {
+    const int64_t lo = (int64_t)q0 - (int64_t)p.mask.window_size;
+    kbeg = lo > 0 ? (int)(lo / BK) * BK : 0;
+  }
+  const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
+
+  // ---- staging: K and V as 16-byte row chunks, 2 of each per thread.
+  const int8_t* kg = (const int8_t*)p.k.ptr + (int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh;
+  const int8_t* vg = (const int8_t*)p.v.ptr + (int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh;
+  constexpr int KCPR = DP / 16;  // 8 chunks per K row
+  // K/V tiles arrive by LDS-DMA straight into the swizzled layout (mfa_stage.h TileDMA);
+  // rows past the end and columns past D read as zeros (the host requires D % 16 == 0).
+  TileDMA<DP, BK, NT> kd, vd;
+  kd.init((const char*)kg, (int)p.k.ss, p.C, p.D, tid);
+  vd.init((const char*)vg, (int)p.v.ss, p.C, p.D, tid);
+
+  // V^T operand via ds_read_b64_tr_b8: in each 16-lane group, lane 2j supplies the row of key
+  // acc_row(j + 8r, h) at column d0, lane 2j+1 the same row at d0 + 8; lane i < 8 receives
+  // column d0 + i of those 8 rows, lane 8 + i column d0 + 8 + i.
+  const int trj = (lane & 15) >> 1;
+  const int trg = (lane >> 4) & 1;
+  int tr_row[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) tr_row[r] = acc_row(trj + 8 * r, hh);
+  auto read_vt = [&](const char* vt, int j, int dt) -> i32x4 {
+    const int col = dt * 32 + 16 * trg + 8 * (lane & 1);
+    i32x2 v[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const char* pa = vt + TK::off(j * 32 + tr_row[r], col >> 4) + (col & 15);
+      v[r] = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)pa);
+    }
+    return i32x4{v[0][0], v[0][1], v[1][0], v[1][1]};
+  };
+
+  i32x16 oi[DP / 32];
+#pragma unroll
+  for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oi[dt][i] = 0;
+  float m = -kFltMax, lh = 0.f;
+
+  if (kbeg < kend) {
+    kd.issue(kbeg, kb0);
+    vd.issue(kbeg, vb0);
+    wait_vm();
+  }
+  __syncthreads();
+
+  int cur = 0;
+  [[maybe_unused]] i32x4 kfa[4], vfa[3];
+  if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kfa[i] = *reinterpret_cast<const i32x4*>(kb0 + TK::off(l32 + 32 * (i & 1), hh));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vfa[i] = read_vt(vb0, 0, i);
+  }
+  for (int t = kbeg; t < kend; t += BK) {
+    const bool has_next = t + BK < kend;
+    if ((ABL & 1) == 0 && has_next) {  // the other buffer was last read before the previous barrier
+      kd.issue(t + BK, kb0 + (cur ^ 1) * KTILE);
+      vd.issue(t + BK, vb0 + (cur ^ 1) * VTILE);
+    }
+    const char* kt = kb0 + cur * KTILE;
+    const char* vt = vb0 + cur * VTILE;
+
+    i32x16 si[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) si[j][i] = 0;
+    {
+      // K fragments read AH MFMAs ahead; sched_barrier(0) pins the order.
+      constexpr int NM = KSTEPS * NJ, AH = 4;
+      i32x4 kf[AH];
+#pragma unroll
+      for (int i = 0; i < AH; ++i)
+        kf[i] = (ABL & 8) ? kfa[i] : *reinterpret_cast<const i32x4*>(kt + TK::off((i % NJ) * 32 + l32, 2 * (i / NJ) + hh));
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        const int j = i % NJ;
+        si[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(kf[i % AH], qf[i / NJ], si[j], 0, 0, 0);
+        if ((ABL & 8) == 0 && i + AH < NM) {
+          const int n = i + AH;
+          kf[i % AH] = *reinterpret_cast<const i32x4*>(kt + TK::off((n % NJ) * 32 + l32, 2 * (n / NJ) + hh));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    i32x4 pb[NJ];
+    if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) pb[j] = i32x4{si[j][0], si[j][1], si[j][2], si[j][3]};
+    } else {
+    float sf[NJ][16];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sf[j][i] = (float)si[j][i];
+    const bool edge = t + BK > p.C;
+    const bool diag = p.mask.causal && t + BK - 1 > q0;
+    if (edge || diag || p.mask.window) {
+      MFA_KEEP_BRANCH();
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = t + j * 32 + acc_row(i, hh);
+          if ((p.mask.causal && key > qi) || (p.mask.window && qi - key > wsz)) sf[j][i] = kMaskValue;
+          if (key >= p.C) sf[j][i] = -__builtin_inff();
+        }
+    }
+    float mx = sf[0][0];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sf[j][i]);
+    const float m_tile = xh_max(mx) * cq;
+    // The running max is kept integer-valued (rounded up), so a rescale multiplies O_int by
+    // an exact power of two: one arithmetic shift per accumulator instead of a float round
+    // trip.  P' keeps at least 6 of its 7 bits (the rounded max exceeds the true one by < 1).
+    if (__any(m_tile > m)) {
+      const float m_new = fmaxf(m, ceilf(m_tile));
+      const float dm = m_new - m;
+      lh *= __builtin_amdgcn_exp2f(-dm);
+      m = m_new;
+      const int k = dm >= 31.f ? 32 : (int)dm;
+      if (__any(k != 0)) {
+#pragma unroll
+        for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oi[dt][i] = k >= 32 ? 0 : (oi[dt][i] >> k);
+      }
+    }
+    // P' = 127 P = exp2(s*c - (m - log2 127)) in [0, 127]; v_cvt_pk_u8_f32 rounds it into
+    // byte e of the packed B operand.  l accumulates P' (the 127 cancels in O = Σ P'v / Σ P').
+    const float mq = m - 6.98868468677217f;  // log2(127)
+    float (&ps)[NJ][16] = sf;
+    if (__any(m < kMaskLevel)) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ps[j][i] = __builtin_amdgcn_exp2f(mul_rn(sf[j][i], cq) - mq);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ps[j][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sf[j][i], cq, -mq));
+    }
+    float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rs[e] += ps[j][4 * k + e];
+          word = __builtin_amdgcn_cvt_pk_u8_f32(ps[j][4 * k + e], e, word);
+        }
+        pb[j][k] = (int)word;
+      }
+    lh += (rs[0] + rs[1]) + (rs[2] + rs[3]);
+    }
+    {
+      // O^T += V^T · P'^T (k order = accumulator registers); V^T fragments AH MFMAs ahead.
+      constexpr int ND = DP / 32, NM = NJ * ND, AH = 3;
+      i32x4 vf[AH];
+#pragma unroll
+      for (int i = 0; i < AH; ++i) vf[i] = (ABL & 8) ? vfa[i] : read_vt(vt, i / ND, i % ND);
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        oi[i % ND] = __builtin_amdgcn_mfma_i32_32x32x32_i8(vf[i % AH], pb[i / ND], oi[i % ND], 0, 0, 0);
+        if ((ABL & 8) == 0 && i + AH < NM) vf[i % AH] = read_vt(vt, (i + AH) / ND, (i + AH) % ND);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    if constexpr ((ABL & 2) == 0) {
+      wait_vm();
+      __syncthreads();
+    }
+    cur ^= 1;
+  }
+
+  float l = xh_sum(lh);
+  if (!(l > 0.f)) l = kFltMin;
+  if constexpr (NG == 2) {
+    // Both blocks' O leave through LDS row images (one per group, over the free K/V ring and
+    // above it) as whole rows from all 8 waves, by non-temporal stores (as the fp16
+    // shared-tile kernel; O is written once).
+    constexpr int ORS = DP * 4 + 16, CPR = DP / 4, OST = BQ * CPR / NT;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const float inv = p.o_mul / l;
+    char* orow = smem + (grp * BQ + wave * 32 + l32) * ORS;
+#pragma unroll
+    for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f4v*>(orow + (dt * 32 + 8 * g + 4 * hh) * 4) =
+            f4v{(float)oi[dt][4 * g] * inv, (float)oi[dt][4 * g + 1] * inv,
+                (float)oi[dt][4 * g + 2] * inv, (float)oi[dt][4 * g + 3] * inv};
+    if (hh == 0 && qvalid) {
+      const float L = m + __log2f(l) - 6.98868468677217f;
+      const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
+      if (p.l_f16)
+        reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+      else
+        reinterpret_cast<float*>(p.l)[li] = L;
+    }
+    __syncthreads();
+    float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+    const int qb0 = NG * (bid / BH) * BQ;
+#pragma unroll
+    for (int blk = 0; blk < NG; ++blk) {
+      const int qb = qb0 + blk * BQ;
+      store_o_image<DP, BQ, NT, true>(p, obase, smem + blk * BQ * ORS, ORS, qb, tid,
+                                      qb + BQ <= p.R && p.D == DP);
+    }
+    return;
+  }
+  if (qvalid) {
+    const float inv = p.o_mul / l;
+    float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)qi * p.o_ss;
+#pragma unroll
+    for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        if (d < p.D)
+          *reinterpret_cast<float4*>(orow + d) =
+              make_float4((float)oi[dt][4 * g] * inv, (float)oi[dt][4 * g + 1] * inv,
+                          (float)oi[dt][4 * g + 2] * inv, (float)oi[dt][4 * g + 3] * inv);
+      }
+    if (hh == 0) {
+      const float L = m + __log2f(l) - 6.98868468677217f;
+      const int64_t li = (int64_t)(b * p.H + h) * p.R + qi;
+      if (p.l_f16)
+        reinterpret_cast<uint16_t*>(p.l)[li] = f32_to_f16(L);
+      else
+        reinterpret_cast<float*>(p.l)[li] = L;
+    }
+  }
+}
+
+template <int ABL>
+__global__ void __launch_bounds__(512, 2) mfa_fwd_i8_abl_kernel(FwdParams p) {
+  mfa_fwd_i8_body<F16, 128, 128, 2, 2, ABL>(p);
+}
+
+}  // namespace diag
+}  // namespace mfa

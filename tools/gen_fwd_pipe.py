@@ -54,6 +54,11 @@ def r(a, b=None):
     return f"v{a}" if b is None else f"v[{a}:{b}]"
 
 
+# Ablation switches (timing-only diagnostic builds, tools/diag/pipe_abl.hip): drop every LDS
+# fragment read and its waits (NOLDS) or the exp / row-sum / pack work (NOEXP).
+ABL = {"nolds": False, "noexp": False}
+
+
 class Block:
     """Instruction list with LDS-wait and MFMA-hazard bookkeeping."""
 
@@ -71,10 +76,14 @@ class Block:
             self.states += 1
 
     def lds_read(self, text, tag):
+        if ABL["nolds"]:
+            return
         self.emit(text, "lds")
         self.lds.append(tag)
 
     def wait_lds(self, tag):
+        if ABL["nolds"]:
+            return
         # Wait until the read `tag` has returned: the reads issued after it may stay in flight.
         n = len(self.lds) - 1 - self.lds.index(tag)
         self.emit(f"s_waitcnt lgkmcnt({min(n, 15)})", "wait")
@@ -126,6 +135,60 @@ def exp_work(cur):
     return w
 
 
+# Balanced schedule (BAL): the exponentials of a tile are split between the two blocks.  The Y
+# block of step t computes P = exp2(S'(t+1)) for s[0] of tile t+1 out of place, into the K
+# fragment ring (free during Y), beside the row max — speculatively, against the current
+# offset, since the rescale decision follows the block (a rescale recomputes them from the
+# shifted S').  The X block of step t+1 packs those first (before its K reads reuse the ring),
+# then exponentiates s[1] in place.  The row-sum partials run in fwd2_exp's order across the
+# two blocks, so the results are bit-identical to the compiler-scheduled kernels.
+BAL = True
+
+
+def exp_y_work(nxt):
+    """Y block: P of s[0] of S(t+1) into KR (v64..v79) and its row-sum partials (started)."""
+    w = []
+    base = SBUF[nxt][0]
+    for pr in range(8):
+        a, b = 2 * pr, 2 * pr + 1
+        w.append((f"v_exp_f32 {r(KR[0] + a)}, {r(base + a)}", (base + a,), 2))
+        w.append((f"v_exp_f32 {r(KR[0] + b)}, {r(base + b)}", (base + b,), 2))
+        for i in (a, b):
+            ra = RS + (i & 3)
+            src = "0" if i < 4 else r(ra)
+            w.append((f"v_add_f32 {r(ra)}, {src}, {r(KR[0] + i)}", (), 1))
+    return w
+
+
+def pack_s0_work(cur):
+    """X block prelude: P[0], P[1] of tile t (s[0], computed by the previous Y block into KR)
+    packed to fp16 into s[0]'s registers 0..3 and 8..11."""
+    base = SBUF[cur][0]
+    w = []
+    for ks in range(2):
+        for pr in range(4):
+            a = KR[0] + 8 * ks + 2 * pr
+            w.append((f"v_cvt_pk_f16_f32 {r(base + 8 * ks + pr)}, {r(a)}, {r(a + 1)}", (), 1))
+    return w
+
+
+def exp_x_work(cur):
+    """X block: exp2 of s[1] of tile t in place, row-sum partials continued, fp16 pack."""
+    w = []
+    base = SBUF[cur][1]
+    for ks in range(2):
+        g = base + 8 * ks
+        for pr in range(4):
+            a, b = g + 2 * pr, g + 2 * pr + 1
+            w.append((f"v_exp_f32 {r(a)}, {r(a)}", (a,), 2))
+            w.append((f"v_exp_f32 {r(b)}, {r(b)}", (b,), 2))
+            for x in (a, b):
+                ra = RS + ((x - base) & 3)
+                w.append((f"v_add_f32 {r(ra)}, {r(ra)}, {r(x)}", (), 1))
+            w.append((f"v_cvt_pk_f16_f32 {r(g + pr)}, {r(a)}, {r(b)}", (), 1))
+    return w
+
+
 def max_work(nxt):
     """Row max of S(t+1): two v_max3 chains (s[0] into mx, s[1] into mt), interleaved so the
     two dependency chains run side by side; the caller ends with max(mx, mt).  A list of
@@ -171,20 +234,34 @@ def v_frag(i, vslot):
             f"ds_read_b64_tr_b16 {r(reg + 2, reg + 3)}, %[va1] offset:{o + RB}", reg)
 
 
-def gen_x(par, qk, ex):
+# MFMA gaps of the X block that issue the step's four LDS-DMA pieces (dma variant): K(t+2)
+# pieces 0/1 and V(t+1) pieces 0/1 of this wave (DmaA<128, 64, 512>: two pieces per operand).
+DMA_GAPS = {1: ("kd", "ko0", "kl0"), 4: ("kd", "ko1", "kl1"), 7: ("vd", "vo0", "vl0"),
+            10: ("vd", "vo1", "vl1")}
+
+
+def gen_x(par, qk, ex, dma=False):
     """X block of step parity par: QK^T(t+1) (qk) with exp/pack of S(t) (ex); ends with the
-    first three V(t) fragment reads when ex (the PV of this step follows)."""
+    first three V(t) fragment reads when ex (the PV of this step follows).  dma: the step's
+    LDS-DMA pieces ride in the MFMA gaps (DMA_GAPS) instead of being issued before the block."""
     kslot, vslot = par ^ 1, par
     cur, nxt = (1, 0) if par else (0, 1)
     b = Block()
-    work = exp_work(cur) if ex else []
+    if BAL:
+        work = exp_x_work(cur) if ex and not ABL["noexp"] else []
+        if ex:
+            # P[0], P[1] out of the K ring before the K reads reuse it.
+            for t, rd, _ in pack_s0_work(cur):
+                b.valu(t, rd)
+    else:
+        work = exp_work(cur) if ex and not ABL["noexp"] else []
     wi = 0
     if qk:
         for i in range(4):
             t, _ = k_frag(i, kslot)
             b.lds_read(t, ("k", i))
         # Exponentials first while the first K fragments land.
-        pre = 10 if ex else 0
+        pre = min(10, len(work))
         for _ in range(pre):
             t, rd, _ = work[wi]
             b.valu(t, rd)
@@ -199,6 +276,11 @@ def gen_x(par, qk, ex):
             if i + 4 < 16:
                 t, _ = k_frag(i + 4, kslot)
                 b.lds_read(t, ("k", i + 4))
+            if dma and i in DMA_GAPS:
+                d, o, l = DMA_GAPS[i]
+                b.emit(f"s_mov_b32 m0, %[{l}]", "salu")
+                b.emit("s_nop 0", "nop")
+                b.emit(f"buffer_load_dwordx4 %[{o}], %[{d}], 0 offen lds", "vmem")
             acc += per
             while wi < len(work) and wi < round(acc) + pre:
                 t, rd, _ = work[wi]
@@ -234,6 +316,21 @@ def gen_y(par, pv, mx, trail=(0, 0)):
     cur, nxt = (1, 0) if par else (0, 1)
     b = Block()
     work = max_work(nxt) if mx else []
+    if mx and BAL and not ABL["noexp"]:
+        # Max chains and the speculative exponentials of s[0] side by side (independent: the
+        # exponentials go out of place).
+        ew = exp_y_work(nxt)
+        merged = []
+        mi = ei = 0
+        while mi < len(work) or ei < len(ew):
+            if mi < len(work):
+                merged.append(work[mi])
+                mi += 1
+            for _ in range(2):
+                if ei < len(ew):
+                    merged.append(ew[ei])
+                    ei += 1
+        work = merged
     if mx:
         # The QK^T results were written by the X block's last MFMAs: the reads below are
         # padded by their distance from those MFMAs (code between the blocks only adds).
@@ -243,7 +340,7 @@ def gen_y(par, pv, mx, trail=(0, 0)):
     wi = 0
     if pv:
         # Fragments 0..2 were issued by the X block (tags continue from there).
-        for i in range(3):
+        for i in range(3 if not ABL["nolds"] else 0):
             b.lds.append(("v", i, 0))
             b.lds.append(("v", i, 1))
         for i in range(16):
@@ -255,11 +352,13 @@ def gen_y(par, pv, mx, trail=(0, 0)):
                 ta, tb, _ = v_frag(i + 3, vslot)
                 b.lds_read(ta, ("v", i + 3, 0))
                 b.lds_read(tb, ("v", i + 3, 1))
-            # One max3 per gap from gap 1 on (the two chains interleaved).
-            if i >= 1 and wi < len(work):
-                t, rd, _ = work[wi]
-                b.valu(t, rd)
-                wi += 1
+            # From gap 1 on, an even share of the max / exp work per gap.
+            if i >= 1:
+                quota = -(-len(work) * i // 15)
+                while wi < len(work) and wi < quota:
+                    t, rd, _ = work[wi]
+                    b.valu(t, rd)
+                    wi += 1
     while wi < len(work):
         t, rd, _ = work[wi]
         b.valu(t, rd)
@@ -291,6 +390,20 @@ def func(name, block, args, outs=(), inouts=(), extra_clobbers=()):
             + f"               : {clob});\n}}\n")
 
 
+def func_dma(name, block):
+    """The X block with the step's LDS-DMA pieces: two buffer descriptors (K(t+2), V(t+1)),
+    the wave's per-lane offsets and LDS destinations of its two pieces of each."""
+    return (f"__device__ __forceinline__ void {name}(int ka0, int ka1, int va0, int va1, float& lh,\n"
+            "    const DmaPieces& dp) {\n"
+            + f"  asm volatile(\"{block.text()}\"\n"
+            + "               : [lh] \"+v\"(lh)\n"
+            + "               : [ka0] \"v\"(ka0), [ka1] \"v\"(ka1), [va0] \"v\"(va0), [va1] \"v\"(va1),\n"
+            + "                 [kd] \"s\"(dp.kd), [vd] \"s\"(dp.vd), [ko0] \"v\"(dp.ko0), [ko1] \"v\"(dp.ko1),\n"
+            + "                 [vo0] \"v\"(dp.vo0), [vo1] \"v\"(dp.vo1), [kl0] \"s\"(dp.kl0), [kl1] \"s\"(dp.kl1),\n"
+            + "                 [vl0] \"s\"(dp.vl0), [vl1] \"s\"(dp.vl1)\n"
+            + f"               : {CLOBBER_MACRO}, \"m0\", \"memory\");\n}}\n")
+
+
 def lh_fold(b):
     """lh += (rs0 + rs1) + (rs2 + rs3), fwd2_exp's order."""
     b.emit(f"v_add_f32 {r(RS)}, {r(RS)}, {r(RS + 1)}", "valu")
@@ -313,6 +426,10 @@ def gen_rescale(par):
             b.emit(f"v_sub_f32 {r(base + k)}, {r(base + k)}, %[shift]", "valu")
     for k in range(16):
         b.emit(f"v_mov_b32 {r(NEGM + k)}, %[negm]", "valu")
+    if BAL:
+        # The Y block's speculative P of s[0] (and its row-sum partials) from the shifted S'.
+        for t, rd, _ in exp_y_work(nxt):
+            b.emit(t, "valu")
     return b
 
 
@@ -343,6 +460,15 @@ def main():
            "#define MFA_PIPE_CLOBBERS " + ", ".join(f'"v{k}"' for k in range(48, 256)),
            "",
            "namespace mfa {",
+           "",
+           "typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));",
+           "// The LDS-DMA operands of one step (pipe_x_qk_exp_dma_*): buffer descriptors of K(t+2) and",
+           "// V(t+1), this wave's per-lane offsets and LDS destinations of its two pieces of each.",
+           "struct DmaPieces {",
+           "  u32x4_t kd, vd;",
+           "  int ko0, ko1, vo0, vo1;",
+           "  unsigned kl0, kl1, vl0, vl1;",
+           "};",
            ""]
     for par in (0, 1):
         for qk, ex, tag in ((1, 1, "qk_exp"), (1, 0, "qk"), (0, 1, "exp")):
@@ -351,6 +477,9 @@ def main():
                 lh_fold(b)
             args = (["ka0", "ka1"] if qk else []) + (["va0", "va1"] if ex else [])
             out.append(func(f"pipe_x_{tag}_{par}", b, args, inouts=["lh"] if ex else []))
+        b = gen_x(par, 1, 1, dma=True)
+        lh_fold(b)
+        out.append(func_dma(f"pipe_x_qk_exp_dma_{par}", b))
         nxt = 0 if par else 1
         xqe, xq = gen_x(par, 1, 1), gen_x(par, 1, 0)
         lh_fold(xqe)
@@ -383,6 +512,38 @@ def main():
                        "metal-flash-attention-plus_amd", "csrc", "fwd_pipe_asm.h")
     open(dst, "w").write("\n".join(out) + "\n")
     print("wrote", os.path.normpath(dst))
+    # Ablation variants of the two steady-state blocks for the diagnostic build.
+    abl = ["// Generated by tools/gen_fwd_pipe.py: timing-only ablations of the steady blocks",
+           "// (tools/diag/pipe_abl.hip).  Wrong results by construction.", "#pragma once",
+           '#include "../../metal-flash-attention-plus_amd/csrc/fwd_pipe_asm.h"', "",
+           "namespace mfa {", ""]
+    for code, flags in ((4, dict(noexp=True)), (8, dict(nolds=True)),
+                        (12, dict(noexp=True, nolds=True))):
+        ABL.update(nolds=False, noexp=False)
+        ABL.update(flags)
+        for par in (0, 1):
+            b = gen_x(par, 1, 1)
+            lh_fold(b)
+            abl.append(func(f"pipe_x_qk_exp_{par}_a{code}", b, ["ka0", "ka1", "va0", "va1"],
+                            inouts=["lh"]))
+            b = gen_y(par, 1, 1, (16, 16))
+            text = func(f"pipe_y_pv_max_{par}_a{code}", b, ["va0", "va1"], outs=["mx", "mt"])
+            text = text.replace(", float& mt)", ")").replace(
+                " {\n  asm volatile", " {\n  float mt;\n  asm volatile", 1)
+            abl.append(text)
+    ABL.update(nolds=False, noexp=False)
+    for par in (0, 1):
+        for nm, sig, call in ((f"pipe_x_qk_exp_{par}", "int ka0, int ka1, int va0, int va1, float& lh",
+                               "ka0, ka1, va0, va1, lh"),
+                              (f"pipe_y_pv_max_{par}", "int va0, int va1, float& mx", "va0, va1, mx")):
+            abl.append(f"template <int A> __device__ __forceinline__ void {nm}_a({sig}) {{")
+            for code in (4, 8, 12):
+                abl.append(f"  if constexpr (A == {code}) {nm}_a{code}({call});")
+            abl.append("}")
+    abl.append("}  // namespace mfa")
+    dst2 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "diag", "fwd_pipe_asm_abl.h")
+    open(dst2, "w").write("\n".join(abl) + "\n")
+    print("wrote", os.path.normpath(dst2))
 
 
 if __name__ == "__main__":
