@@ -28,6 +28,7 @@
 // exp2(S·c − L) needs no mask-level special case.
 #include "mfa_stage.h"
 #include "mfa_dispatch.h"
+#include "kv_bytes.h"
 
 namespace mfa {
 
@@ -167,14 +168,24 @@ __device__ __forceinline__ void tr_chain(const char* tile, const int (&trb)[2], 
 
 // ---------------------------------------------------------------------------------------
 // backwardQuery.  Grid: nblk x B x H, heaviest causal blocks first.  BT keys per tile.
-template <class E, int DP, int BT, bool MSK = false>
+// KVQ: K/V storage — SRC_SAME (16-bit, LDS-DMA into the ring), or SRC_I8 / SRC_I4 per-tensor
+// quantised: the stored bytes of tile t + 2 move by LDS-DMA into a byte ring (kv_bytes.h) at
+// the top of step t, and tile t + 1's bytes are widened into its 16-bit slot between the S
+// chain's MFMAs (which carry no other VALU work), so the MFMA operands are those of the
+// dequantisation pass + 16-bit kernel path, without the pass or its scratch copy.
+template <class E, int DP, int BT, bool MSK = false, int KVQ = SRC_SAME>
 __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   using A = Arith16<E, DP>;
   constexpr int NT = 256, BQ = 128, NJ = BT / 32, DS = DP / 16, ND = DP / 32;
   constexpr int TILEB = BT * DP * 2;
+  constexpr bool QKV = KVQ != SRC_SAME;
+  static_assert(!(QKV && MSK), "quantised K/V: no element-wise mask instantiation");
+  using KB = KvBytes<E, DP, BT, QKV ? KVQ : SRC_I8, NT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const kb0 = smem;
   char* const vb0 = smem + 2 * TILEB;
+  char* const rawk = smem + 4 * TILEB;       // QKV: byte ring, K slots 0, 1 then V slots 0, 1
+  char* const rawv = rawk + 2 * KB::SLOT;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -259,13 +270,36 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     tin_hi = imn;
   }
   DmaA<DP, BT, NT> kd, vd;
-  kd.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
-  vd.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
-  const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
-  const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
-  if (kbeg < kend) {
-    kd.issue(khead, kbeg, kb0);
-    vd.issue(vhead, kbeg, vb0);
+  KB kq, vq;
+  // Element offsets -> byte offsets: 16-bit x 2, INT8 x 1, INT4 / 2.
+  auto head_bytes = [&](const Operand& op) {
+    const int64_t e = (int64_t)b * op.sb + (int64_t)kvh * op.sh;
+    return (const char*)op.ptr + (QKV ? e >> KB::SH : e * 2);
+  };
+  const char* khead = head_bytes(p.k);
+  const char* vhead = head_bytes(p.v);
+  const int kss = QKV ? (int)(p.k.ss >> KB::SH) : 0, vss = QKV ? (int)(p.v.ss >> KB::SH) : 0;
+  const int kbytes = QKV ? (int)((int64_t)(p.C - 1) * kss + (p.D >> KB::SH)) : 0;
+  const int vbytes = QKV ? (int)((int64_t)(p.C - 1) * vss + (p.D >> KB::SH)) : 0;
+  const float zk = (float)p.k.zp, zv = (float)p.v.zp;
+  if constexpr (QKV) {
+    kq.init(tid, p.D, kss);
+    vq.init(tid, p.D, vss);
+    if (kbeg < kend) {
+      kq.dma(khead, kss, kbytes, kbeg, rawk);
+      vq.dma(vhead, vss, vbytes, kbeg, rawv);
+      if (kbeg + BT < kend) {
+        kq.dma(khead, kss, kbytes, kbeg + BT, rawk + KB::SLOT);
+        vq.dma(vhead, vss, vbytes, kbeg + BT, rawv + KB::SLOT);
+      }
+    }
+  } else {
+    kd.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
+    vd.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
+    if (kbeg < kend) {
+      kd.issue(khead, kbeg, kb0);
+      vd.issue(vhead, kbeg, vb0);
+    }
   }
 
   // D = scale · Σ_d dO∘O (computeD, Softmax.swift:31-236): dO as stored (16-bit), O fp32.
@@ -315,10 +349,27 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   for (int dt = 0; dt < ND; ++dt) dq[dt] = zero16();
 
   wait_vm();
+  if constexpr (QKV) {
+    // The first tile's bytes are in (the second's may be too): widen the first.
+    __asm__ __volatile__("" ::: "memory");
+    if (kbeg < kend) {
+#pragma unroll
+      for (int m = 0; m < KB::NPIECE; ++m) {
+        kq.widen(kb0, kq.read(rawk, m), zk, m, p.C - kbeg);
+        vq.widen(vb0, vq.read(rawv, m), zv, m, p.C - kbeg);
+      }
+    }
+  }
   __syncthreads();
   int cur = 0;
   for (int t = kbeg; t < kend; t += BT) {
-    if (t + BT < kend) {
+    if constexpr (QKV) {
+      // Tile t + 2's bytes into the byte slot tile t's left (widened during the last step).
+      if (t + 2 * BT < kend) {
+        kq.dma(khead, kss, kbytes, t + 2 * BT, rawk + cur * KB::SLOT);
+        vq.dma(vhead, vss, vbytes, t + 2 * BT, rawv + cur * KB::SLOT);
+      }
+    } else if (t + BT < kend) {
       kd.issue(khead, t + BT, kb0 + (cur ^ 1) * TILEB);
       vd.issue(vhead, t + BT, vb0 + (cur ^ 1) * TILEB);
     }
@@ -349,7 +400,36 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
           }
       }
     }
-    rows_chain<A, NJ>(kt, qf, s, rbase, [](int) {});
+    if constexpr (QKV) {
+      // Tile t + 1 widened piece by piece under the S chain, which carries no other VALU work:
+      // 2·NPIECE pieces (K and V), one after every EVERY-th MFMA, each piece's bytes read into
+      // registers before the chain so no widening waits on its LDS read.
+      constexpr int NM = DS * NJ, NPW = 2 * KB::NPIECE, EVERY = NM / NPW;
+      static_assert(NM % NPW == 0 && EVERY >= 1, "widening slots");
+      const bool wnext = t + BT < kend;
+      const int nrows = p.C - (t + BT);
+      const char* rk = rawk + (cur ^ 1) * KB::SLOT;
+      const char* rv = rawv + (cur ^ 1) * KB::SLOT;
+      char* const kn = kb0 + (cur ^ 1) * TILEB;
+      char* const vn = vb0 + (cur ^ 1) * TILEB;
+      // Piece w: K piece w / 2 (w even) or V piece w / 2 (w odd).
+      uint4 raws[NPW];
+#pragma unroll
+      for (int w = 0; w < NPW; ++w)
+        raws[w] = wnext ? ((w & 1) ? vq.read(rv, w >> 1) : kq.read(rk, w >> 1))
+                        : make_uint4(0u, 0u, 0u, 0u);
+      rows_chain<A, NJ>(kt, qf, s, rbase, [&](int i) {
+        if (i % EVERY == EVERY - 1 && wnext) {
+          const int w = i / EVERY;
+          if (w & 1)
+            vq.widen(vn, raws[w], zv, w >> 1, nrows);
+          else
+            kq.widen(kn, raws[w], zk, w >> 1, nrows);
+        }
+      });
+    } else {
+      rows_chain<A, NJ>(kt, qf, s, rbase, [](int) {});
+    }
     if constexpr (MSK) {
       if (t >= tin_lo && min(t + BT, p.C) <= tin_hi) {
         if (p.mask.amask) {
@@ -965,6 +1045,18 @@ static hipError_t launch_bwd_q_fast(const BwdParams& p, hipStream_t stream) {
   BwdParams q = p;
   q.nblk = (p.R + 127) / 128;
   const dim3 grid(q.nblk * p.B * p.H);
+  if (p.k.prec == P_INT8 || p.k.prec == P_INT4) {
+    // Quantised K/V widened on load: the 16-bit ring plus the byte ring (4 tiles of bytes).
+    if (p.mask.amask || p.mask.ranges || p.v.prec != p.k.prec) return hipErrorNotSupported;
+    if (p.k.prec == P_INT8) {
+      using KB = KvBytes<E, DP, BT, SRC_I8, 256>;
+      return launch(mfa_bwd_q_fast_kernel<E, DP, BT, false, SRC_I8>, grid, dim3(256),
+                    LDS + 4 * KB::SLOT, stream, q);
+    }
+    using KB = KvBytes<E, DP, BT, SRC_I4, 256>;
+    return launch(mfa_bwd_q_fast_kernel<E, DP, BT, false, SRC_I4>, grid, dim3(256),
+                  LDS + 4 * KB::SLOT, stream, q);
+  }
   if (p.mask.amask || p.mask.ranges)
     return launch(mfa_bwd_q_fast_kernel<E, DP, BT, true>, grid, dim3(256), LDS + 128, stream, q);
   return launch(mfa_bwd_q_fast_kernel<E, DP, BT>, grid, dim3(256), LDS, stream, q);
@@ -1014,6 +1106,8 @@ namespace mfa {
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I8>(BwdParams); \
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_I4>(BwdParams); \
   template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, true>(BwdParams);   \
+  template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, false, SRC_I8>(BwdParams); \
+  template __global__ void mfa_bwd_q_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BT, false, SRC_I4>(BwdParams); \
   template __global__ void mfa_bwd_kv_fast_kernel<EE, DPV, BwdFastCfg<DPV>::BQ, SRC_SAME, true>(BwdParams);
 MFA_BF_INST(F16, 64)
 MFA_BF_INST(F16, 128)

@@ -14,39 +14,38 @@
 //     (global loads, about one step of latency cover; no LDS staging, so the LDS traffic is
 //     the 16-bit kernel's);
 //   - runs tile s from its 16-bit image exactly as the 16-bit kernel does.
+// Instantiated for FP16 and BF16 at D = 64, 128 (BK = 64) and 256 (BK = 32, the 16-bit
+// kernel's tile depth there; one 16-byte chunk per thread per tile at every width but 64,
+// where each thread widens one 8-element chunk).
 // Per-tensor scales stay folded in the softmax multiplier (K) and the output multiplier (V),
 // so the MFMA operands, and hence O and L, are bit-identical to the dequantise pass +
 // 16-bit kernel path — with 1 byte (INT4: half a byte) per K/V element read from HBM, no
 // pass, no scratch.
-// LDS: 16-bit ring 4 x 16 KiB, reused at the end for the two O row images
-// (2 x 128 rows x (4·D + 16) bytes).
+// LDS: 16-bit ring of 4 tiles, reused at the end for the two O row images
+// (2 x 128 rows x (4·D + 16) bytes) up to D = 128; at D = 256 rows leave from registers.
 #include "attention_fwd2.h"
+#include "kv_bytes.h"
 
 namespace mfa {
 
-// 8 quantised elements (row r, columns 16c + 8·HALF ..+7) -> one 16-byte chunk of the TileA
-// image.
-// INT8: raw holds 16 bytes (half h: dwords 2h, 2h+1); INT4: 16 nibbles in raw.x, raw.y
-// (half h: dword h, element 2i in the low nibble).
-template <class E, int DP, int SRC, int HALF>
-__device__ __forceinline__ void widen_store(char* img, int r, int c, const uint4 raw, float zp) {
-  uint4 q;
-  if constexpr (SRC == SRC_I8)
-    q = HALF ? make_uint4(raw.z, raw.w, 0u, 0u) : make_uint4(raw.x, raw.y, 0u, 0u);
-  else
-    q = make_uint4(HALF ? raw.y : raw.x, 0u, 0u, 0u);
-  *reinterpret_cast<uint4*>(img + TileA<DP>::off(r, 2 * c + HALF)) = dequant_fast<E, SRC>(q, zp);
-}
-
-template <class E, int DP, int BK, int SRC, int KP0 = 1, int KP1 = 3, int VP0 = 12, int VP1 = 14>
+template <class E, int DP, int BK, int SRC>
 __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   constexpr int NT = 512, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
-  constexpr int CPR = DP / 4;               // 16-byte O chunks per row
-  constexpr int OST = BQ * CPR / NT;        // O stores per thread per block
   constexpr int ORS = DP * 4 + 16;          // O row image stride
-  constexpr int C8 = DP / 16;               // 16-byte INT8 chunks per row
-  static_assert(BK * C8 == NT, "one INT8 chunk of K and of V per thread per tile");
+  constexpr bool OIMG = 2 * 128 * ORS <= 160 * 1024;  // O leaves through row images (D <= 128)
+  using G = Kv8Geo<DP, BK>;
+  constexpr int CE = G::CE;
+  // Widening pieces: after QKᵀ MFMAs 1 and 3 (K) and 4 / 2 before the end of the PV chain (V);
+  // one TileA chunk each (CE = 16), or the single chunk at the second slot (CE = 8).
+  constexpr int NMK = (BK / 32) * (DP / 16), NMV = (BK / 32) * 2 * ND;
+  constexpr int KP0 = 1, KP1 = 3, VP0 = NMV - 4, VP1 = NMV - 2;
+  static_assert(KP1 < NMK && VP0 >= 0, "hook slots");
+  // D = 256: the Q fragments and O accumulators leave no registers for the next tile's bytes
+  // (the register-staged form spills), so the bytes go through an LDS ring by LDS-DMA instead:
+  // each lane's own chunk (one 16-byte piece, or two 4-byte pieces for INT4), read back by the
+  // same lane just before its widening — a counted vmcnt wait, no barrier.
+  constexpr bool RAWLDS = DP == 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -70,51 +69,107 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> ESH);
   const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> ESH);
   const int n = (p.C + BK - 1) / BK;
-  // This thread's 16-byte INT8 chunk of a tile: wave w covers rows 8w..8w+7; 16 consecutive
-  // lanes take the 8 rows x 2 chunk parities, so each 16-byte write into the TileA image
-  // (bank group 4·(r & 3) + ((chunk & 3) ^ ((r >> 2) & 3))) hits 16 distinct bank groups.
-  static_assert(C8 == 8, "8 chunks per row");
-  const int cr = (tid >> 6) * 8 + (lane & 7);
-  const int cc = ((lane >> 3) & 1) | ((lane >> 4) << 1);
-  const bool cvalid = cc * 16 < p.D;
+  const G geo(tid);
+  const int cr = geo.r, ch0 = geo.ch0;
+  const bool cvalid = geo.col < p.D;
   // Range-checked buffer loads: rows past C and chunks past D read as zeros.
-  // Byte geometry: INT8 one byte per element, INT4 half a byte (16-element chunk: 16 / 8 B).
-  constexpr int SH = SRC == SRC_I8 ? 0 : 1, CB = 16 >> SH;
+  // Byte geometry: INT8 one byte per element, INT4 half a byte.
+  constexpr int SH = ESH, CB = CE >> SH;
   const int kss = (int)(p.k.ss >> SH), vss = (int)(p.v.ss >> SH);
   const int kbytes = (int)((int64_t)(p.C - 1) * kss + (p.D >> SH));
   const int vbytes = (int)((int64_t)(p.C - 1) * vss + (p.D >> SH));
-  const int kro = cvalid ? cr * kss + cc * CB : 0x40000000;
-  const int vro = cvalid ? cr * vss + cc * CB : 0x40000000;
+  const int kro = cvalid ? cr * kss + (geo.col >> SH) : 0x40000000;
+  const int vro = cvalid ? cr * vss + (geo.col >> SH) : 0x40000000;
   // This thread's chunk of tile t's K (V) bytes.
   auto load1 = [&](const char* head, int ss, int bytes, int ro, int t) -> uint4 {
     const int tb = t * ss;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(head + tb), (short)0, max(bytes - tb, 0), 0x00020000);
-    if constexpr (SRC == SRC_I8) {
+    if constexpr (CB == 16) {
       const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, ro, 0, 0);
       return make_uint4(a[0], a[1], a[2], a[3]);
-    } else {
+    } else if constexpr (CB == 8) {
       const auto a = __builtin_amdgcn_raw_buffer_load_b64(rs, ro, 0, 0);
       return make_uint4(a[0], a[1], 0u, 0u);
+    } else {
+      return make_uint4(__builtin_amdgcn_raw_buffer_load_b32(rs, ro, 0, 0), 0u, 0u, 0u);
     }
   };
   auto loadk = [&](int t) { return load1(khead, kss, kbytes, kro, t); };
   auto loadv = [&](int t) { return load1(vhead, vss, vbytes, vro, t); };
+  // LDS byte ring (RAWLDS): K slots 0, 1, then V slots 0, 1, of 512 chunks each.
+  constexpr int NPC = CB == 16 ? 1 : CB / 4;  // DMA instructions per operand per tile
+  constexpr int RSLOT = NT * CB;
+  char* const rawb = smem + 4 * TILEB;
+  const int wv = tid >> 6;
+  auto raw_dma = [&](const char* head, int ss, int bytes, int ro, int t, char* slot) {
+    const int tb = t * ss;
+    if constexpr (CB == 16) {
+      lds_dma16(head + tb, max(bytes - tb, 0), ro, slot + wv * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NPC; ++j)
+        lds_dma4(head + tb, max(bytes - tb, 0), ro + 4 * j, slot + j * (NT * 4) + wv * 256);
+    }
+  };
+  // Half hf of this lane's chunk, in the registers half 0 of widen_store reads.
+  auto raw_read = [&](const char* slot, int hf) -> uint4 {
+    if constexpr (CB == 16) {
+      const uint2 a = *reinterpret_cast<const uint2*>(slot + wv * 1024 + lane * 16 + 8 * hf);
+      return make_uint4(a.x, a.y, 0u, 0u);
+    } else {
+      return make_uint4(*reinterpret_cast<const uint32_t*>(slot + hf * (NT * 4) + wv * 256 + lane * 4),
+                        0u, 0u, 0u);
+    }
+  };
+  // Widening of half hf read by raw_read (RAWLDS).
+  auto widen_half = [&](char* img, const uint4& raw, float zp, int hf) {
+    widen_store<E, DP, SRC, 0>(img, cr, ch0 + hf, raw, zp);
+  };
+  auto dmak = [&](int t, int sl) { raw_dma(khead, kss, kbytes, kro, t, rawb + sl * RSLOT); };
+  auto dmav = [&](int t, int sl) { raw_dma(vhead, vss, vbytes, vro, t, rawb + (2 + sl) * RSLOT); };
+  auto widen = [&](char* img, const uint4& raw, float zp, auto half_c) {
+    constexpr int HF = decltype(half_c)::value;
+    widen_store<E, DP, SRC, HF>(img, cr, ch0 + HF, raw, zp);
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
 
   const int q0 = (2 * pi + g) * BQ;
   const int qi = q0 + wg * 32 + l32;
   i16x8 qf[DP / 16];
   // rk / rv: the bytes of the next tile to widen.  Each is reloaded (tile s + 2) as soon as
   // its widening into tile s + 1's slot has been issued, one step ahead of its use.
-  uint4 rk = loadk(0), rv = loadv(0);
-  load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
+  uint4 rk, rv;
+  if constexpr (RAWLDS) {
+    dmak(0, 0);
+    dmav(0, 0);
+    dmak(BK, 1);
+    dmav(BK, 1);
+    load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
+    wait_vm();
+    __asm__ __volatile__("" ::: "memory");
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      widen_half(sk, raw_read(rawb, hf), zk, hf);
+      widen_half(sv, raw_read(rawb + 2 * RSLOT, hf), zv, hf);
+    }
+  } else {
+    rk = loadk(0);
+    rv = loadv(0);
+    load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
+  }
   prescale_q2<E, DP>(qf, c);
-  widen_store<E, DP, SRC, 0>(sk, cr, cc, rk, zk);
-  widen_store<E, DP, SRC, 1>(sk, cr, cc, rk, zk);
-  widen_store<E, DP, SRC, 0>(sv, cr, cc, rv, zv);
-  widen_store<E, DP, SRC, 1>(sv, cr, cc, rv, zv);
-  rk = loadk(BK);
-  rv = loadv(BK);
+  if constexpr (!RAWLDS) {
+    widen(sk, rk, zk, H0());
+    widen(sv, rv, zv, H0());
+    if constexpr (CE == 16) {
+      widen(sk, rk, zk, H1());
+      widen(sv, rv, zv, H1());
+    }
+    rk = loadk(BK);
+    rv = loadv(BK);
+  }
   __syncthreads();
 
   RowState<DP> st;
@@ -131,19 +186,47 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
     i16x8 pb[BK / 16];
     char* const knext = sk + nx * TILEB;
     char* const vnext = sv + nx * TILEB;
-    // The widening in four pieces (5 VALU + one 16-byte LDS write each), one per MFMA gap.
+    // The widening in pieces (5 VALU + one 16-byte LDS write each), one per MFMA gap.
     auto khook = [&](int i) {
-      if (i == KP0) widen_store<E, DP, SRC, 0>(knext, cr, cc, rk, zk);
-      if (i == KP1) {
-        widen_store<E, DP, SRC, 1>(knext, cr, cc, rk, zk);
-        rk = loadk(t + 2 * BK);
+      if constexpr (RAWLDS) {
+        // Tile s + 1's bytes (DMA issued at step s − 1; V(s + 1)'s pieces may still fly).
+        if (i == KP0) {
+          __builtin_amdgcn_s_waitcnt(0x0F70 | NPC);
+          __asm__ __volatile__("" ::: "memory");
+          widen_half(knext, raw_read(rawb + nx * RSLOT, 0), zk, 0);
+        }
+        if (i == KP1) {
+          widen_half(knext, raw_read(rawb + nx * RSLOT, 1), zk, 1);
+          dmak(t + 2 * BK, cur);
+        }
+      } else {
+        if constexpr (CE == 16)
+          if (i == KP0) widen(knext, rk, zk, H0());
+        if (i == KP1) {
+          widen(knext, rk, zk, std::integral_constant<int, CE == 16 ? 1 : 0>());
+          rk = loadk(t + 2 * BK);
+        }
       }
     };
     auto vhook = [&](int i) {
-      if (i == VP0) widen_store<E, DP, SRC, 0>(vnext, cr, cc, rv, zv);
-      if (i == VP1) {
-        widen_store<E, DP, SRC, 1>(vnext, cr, cc, rv, zv);
-        rv = loadv(t + 2 * BK);
+      if constexpr (RAWLDS) {
+        // (K(s + 2)'s pieces, issued above, may still fly.)
+        if (i == VP0) {
+          __builtin_amdgcn_s_waitcnt(0x0F70 | NPC);
+          __asm__ __volatile__("" ::: "memory");
+          widen_half(vnext, raw_read(rawb + (2 + nx) * RSLOT, 0), zv, 0);
+        }
+        if (i == VP1) {
+          widen_half(vnext, raw_read(rawb + (2 + nx) * RSLOT, 1), zv, 1);
+          dmav(t + 2 * BK, cur);
+        }
+      } else {
+        if constexpr (CE == 16)
+          if (i == VP0) widen(vnext, rv, zv, H0());
+        if (i == VP1) {
+          widen(vnext, rv, zv, std::integral_constant<int, CE == 16 ? 1 : 0>());
+          rv = loadv(t + 2 * BK);
+        }
       }
     };
     fwd2_qk<E, DP, BK>(sk + cur * TILEB, rbase, qf, st, sc, khook);
@@ -152,52 +235,77 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
     __syncthreads();
   }
 
-  // Both blocks leave through O row images (one per group) as whole rows from all 8 waves.
   float l = cross_half_sum(st.lh) + kFltMin;
   if (!(l > 0.f)) l = kFltMin;
-  const float inv = p.o_mul / l;
-  char* orow = smem + (g * 128 + wg * 32 + l32) * ORS;
+  if constexpr (!OIMG) {
+    // D = 256: two 128-row images do not fit; rows leave from registers, as the 16-bit
+    // shared-tile kernel's do at this width.
+    if (qi < p.R) store_o_l<DP>(p, st.o, st.m, l, b, h, qi, hh);
+    return;
+  } else {
+    // Both blocks leave through O row images (one per group) as whole rows from all 8 waves.
+    const float inv = p.o_mul / l;
+    char* orow = smem + (g * 128 + wg * 32 + l32) * ORS;
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt)
+    for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq)
-      *reinterpret_cast<float4*>(orow + (dt * 32 + 8 * gq + 4 * hh) * 4) =
-          make_float4(st.o[dt][4 * gq] * inv, st.o[dt][4 * gq + 1] * inv,
-                      st.o[dt][4 * gq + 2] * inv, st.o[dt][4 * gq + 3] * inv);
-  if (hh == 0 && qi < p.R) store_l(p, st.m + __log2f(l), b, h, qi);
-  __syncthreads();
-  float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
+      for (int gq = 0; gq < 4; ++gq)
+        *reinterpret_cast<float4*>(orow + (dt * 32 + 8 * gq + 4 * hh) * 4) =
+            make_float4(st.o[dt][4 * gq] * inv, st.o[dt][4 * gq + 1] * inv,
+                        st.o[dt][4 * gq + 2] * inv, st.o[dt][4 * gq + 3] * inv);
+    if (hh == 0 && qi < p.R) store_l(p, st.m + __log2f(l), b, h, qi);
+    __syncthreads();
+    float* obase = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh;
 #pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int qb = (2 * pi + blk) * BQ;
-    store_o_image<DP, 128, NT, true>(p, obase, smem + blk * 128 * ORS, ORS, qb, tid,
-                                     qb + BQ <= p.R && p.D == DP);
+    for (int blk = 0; blk < 2; ++blk) {
+      const int qb = (2 * pi + blk) * BQ;
+      store_o_image<DP, 128, NT, true>(p, obase, smem + blk * 128 * ORS, ORS, qb, tid,
+                                       qb + BQ <= p.R && p.D == DP);
+    }
   }
 }
 
-size_t fwd_kv8_lds_bytes() {
-  constexpr int DP = 128, BK = 64;
+// (DP, BK) per padded head width: the 16-bit shared-tile kernel's tile depths.
+template <int DP>
+constexpr int kv8_bk() { return DP == 256 ? 32 : 64; }
+
+template <int DP>
+constexpr size_t kv8_lds() {
+  constexpr int BK = kv8_bk<DP>();
   constexpr int RING = 4 * BK * DP * 2;
   constexpr int OIMG = 2 * 128 * (DP * 4 + 16);
-  return RING > OIMG ? RING : OIMG;
+  // D = 256: the ring plus the byte ring (4 slots x 512 chunks of at most 16 bytes).
+  return OIMG > 160 * 1024 ? RING + 4 * 512 * 16 : (RING > OIMG ? RING : OIMG);
 }
 
-hipError_t fwd_kv8_dispatch(const FwdParams& p, int elem, int src, hipStream_t stream) {
-  if (elem != P_FP16) return hipErrorNotSupported;
+size_t fwd_kv8_lds_bytes(int DP) {
+  return DP == 64 ? kv8_lds<64>() : DP == 128 ? kv8_lds<128>() : kv8_lds<256>();
+}
+
+template <class E, int DP>
+static hipError_t launch_kv8(const FwdParams& q, int src, dim3 grid, hipStream_t stream) {
+  constexpr int BK = kv8_bk<DP>();
+  if (src == SRC_I8)
+    return launch(mfa_fwd2_kv8_kernel<E, DP, BK, SRC_I8>, grid, dim3(512), kv8_lds<DP>(), stream, q);
+  if (src == SRC_I4)
+    return launch(mfa_fwd2_kv8_kernel<E, DP, BK, SRC_I4>, grid, dim3(512), kv8_lds<DP>(), stream, q);
+  return hipErrorNotSupported;
+}
+
+hipError_t fwd_kv8_dispatch(const FwdParams& p, int elem, int DP, int src, hipStream_t stream) {
   FwdParams q = p;
   q.nblk = (p.R + 127) / 128;
   const int npairs = (q.nblk + 1) / 2;
   const dim3 grid(npairs * p.B * p.H);
-  const size_t lds = fwd_kv8_lds_bytes();
-  // MFA_KV8_SLOTS=1 (development A/B): the widening pieces at QK^T MFMAs 4 / 10 and PV 4 / 10.
-  const char* sl = mfa::dev_env("MFA_KV8_SLOTS");
-  const bool alt = sl && sl[0] == '1';
-  if (src == SRC_I8)
-    return alt ? launch(mfa_fwd2_kv8_kernel<F16, 128, 64, SRC_I8, 4, 10, 4, 10>, grid, dim3(512), lds, stream, q)
-               : launch(mfa_fwd2_kv8_kernel<F16, 128, 64, SRC_I8>, grid, dim3(512), lds, stream, q);
-  if (src == SRC_I4)
-    return alt ? launch(mfa_fwd2_kv8_kernel<F16, 128, 64, SRC_I4, 4, 10, 4, 10>, grid, dim3(512), lds, stream, q)
-               : launch(mfa_fwd2_kv8_kernel<F16, 128, 64, SRC_I4>, grid, dim3(512), lds, stream, q);
+#define MFA_KV8(ELEM, EE, DPV) \
+  if (elem == ELEM && DP == DPV) return launch_kv8<EE, DPV>(q, src, grid, stream);
+  MFA_KV8(P_FP16, F16, 64)
+  MFA_KV8(P_FP16, F16, 128)
+  MFA_KV8(P_FP16, F16, 256)
+  MFA_KV8(P_BF16, BF16, 64)
+  MFA_KV8(P_BF16, BF16, 128)
+  MFA_KV8(P_BF16, BF16, 256)
+#undef MFA_KV8
   return hipErrorNotSupported;
 }
 

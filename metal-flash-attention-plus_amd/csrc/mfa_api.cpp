@@ -731,18 +731,19 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
   return ((int64_t)p.C * p.k.ss >> sh) < ((int64_t)1 << 31);
 }
 
-// The on-load shared-tile forward (attention_fwd_kv8.hip): FP16 Q, per-tensor INT8 or INT4
-// K/V (any zero point), D % 16 == 0 with D <= 128 padded to 128, no masks, dense rows with
-// 16-byte aligned byte offsets.  MFA_KV8=0 routes these through the dequantisation pass
+// The on-load shared-tile forward (attention_fwd_kv8.hip): FP16 or BF16 Q (the compute type),
+// per-tensor INT8 or INT4 K/V (any zero point), D % 16 == 0 with D <= 256 (padded to 64, 128
+// or 256), no masks, dense rows with 16-byte aligned byte offsets.  MFA_KV8=0 routes these through the dequantisation pass
 // instead (A/B).
 bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int DP) {
   if (const char* e = mfa::dev_env("MFA_KV8")) {
     if (e[0] == '0') return false;
   }
-  if (elem != 1 || qp != MFA_PRECISION_FP16) return false;
+  if (!((elem == 1 && qp == MFA_PRECISION_FP16) || (elem == 2 && qp == MFA_PRECISION_BF16)))
+    return false;
   if (kp != vp || (kp != MFA_PRECISION_INT8 && kp != MFA_PRECISION_INT4)) return false;
   if (p.k.bscale || p.v.bscale) return false;
-  if (DP != 128 || p.D % 16 != 0 || !(p.c_log2 > 0.f)) return false;
+  if ((DP != 64 && DP != 128 && DP != 256) || p.D % 16 != 0 || !(p.c_log2 > 0.f)) return false;
   const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
   if (p.mask.causal || p.mask.window || p.mask.amask || p.mask.ranges) return false;
   if (p.q.sd != 1 || !p.q.vec || p.o_sd != 1) return false;
@@ -878,7 +879,7 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (decode) launch");
   }
   if (kv8_eligible(p, elem, qp, kp, vp, DP))
-    return hip_status(mfa::fwd_kv8_dispatch(p, elem, src_kind(kp), (hipStream_t)stream),
+    return hip_status(mfa::fwd_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream),
                       "mfa_fwd (INT8 K/V on load) launch");
   int kvsrc = src_kind(kp);
   if (dequant_pass_worth(R, H, Hkv, D, elem)) {
@@ -1107,8 +1108,11 @@ bool bwd_fast_eligible(const mfa::BwdParams& p, int elem, int DP, int ksrc, int 
 
 // kv_widen: quantised K/V (16-bit Q) may run the tuned key-phase kernel, which widens them in
 // registers (quantized_backward decides it; false everywhere else).
+// q_widen: the same for the query phase, whose kernel stages the stored K/V bytes through an
+// LDS byte ring and widens them there (kv_bytes.h).
 mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ksrc, int qsrc,
-                          int phase, hipStream_t stream, bool kv_widen = false) {
+                          int phase, hipStream_t stream, bool kv_widen = false,
+                          bool q_widen = false) {
   mfa::BwdParams p = base_p;
   if (mfa_status_t st = check_keys(p.R, p.C)) return st;
   if (p.R == 0)
@@ -1121,9 +1125,10 @@ mfa_status_t run_backward(const mfa::BwdParams& base_p, int elem, int DP, int ks
   if (phase & PHASE_QUERY) {
     p.nblk = (p.R + bp - 1) / bp;
     if (p.R > 0) {
-      hipError_t e = big    ? mfa::bwd_bigd_dispatch(p, 0, elem, stream)
-                     : fast ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream)
-                            : hipErrorNotSupported;
+      const bool fast_q = fast || (!big && ksrc > 0 && q_widen);
+      hipError_t e = big      ? mfa::bwd_bigd_dispatch(p, 0, elem, stream)
+                     : fast_q ? mfa::bwd_fast_dispatch(p, 0, elem, DP, stream)
+                              : hipErrorNotSupported;
       if (big && e == hipErrorNotSupported)
         return fail(MFA_ERR_UNSUPPORTED, "head dimension %d: mixed operand precisions", p.D);
       if (e == hipErrorNotSupported) e = mfa::bwd_q_dispatch(p, elem, DP, ksrc, ksrc, stream);
@@ -1313,7 +1318,25 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
   const char* kvr = mfa::dev_env("MFA_KV_REGS");
   const bool kv_widen = ksrc > 0 && qsrc == 0 && !(kvr && kvr[0] == '0') &&
                         !dequant_pass_needed(D) && bwd_fast_eligible(p, elem, DP, ksrc, qsrc, true);
-  const bool kv_regs = phase == PHASE_KV && kv_widen;
+  // The query phase can take them on load too (LDS byte ring, kv_bytes.h) when the stored rows
+  // suit 16-byte (INT8) / 8-byte (INT4) chunks: per-tensor, D % 16 == 0, 16-byte aligned rows
+  // and heads.  It does so where the pass is not worth running (few query rows per kv head,
+  // where the generic kernel read the quantised K/V before).  Above that the pass stays: that
+  // kernel runs one wave per SIMD, so nothing hides the widening's LDS round trips and VALU,
+  // which every query block repeats for every K/V tile (measured 1.34x the pass path's time at
+  // B4 H32 S4096 D128 INT8, 1.19x at D = 256).  MFA_BWDQ_BYTES=1 / 0 forces
+  // the byte ring / the pass (A/B, bit-identity tests).
+  const char* qb = mfa::dev_env("MFA_BWDQ_BYTES");
+  bool q_widen = kv_widen && D % 16 == 0 &&
+                 (qb ? qb[0] == '1' : !dequant_pass_worth(R, H, Hkv, D, elem));
+  if (q_widen) {
+    const int sh = ksrc == 2 ? 1 : 0;
+    for (const mfa::Operand* o : {&p.k, &p.v})
+      if (o->ss % (16 << sh) || o->sh % (16 << sh) || o->sb % (16 << sh) ||
+          (uintptr_t)o->ptr % 16 || (((int64_t)C + 128) * o->ss >> sh) >= ((int64_t)1 << 31))
+        q_widen = false;
+  }
+  const bool kv_regs = kv_widen && (!(phase & PHASE_QUERY) || q_widen);
   if (dequant_pass_worth(R, H, Hkv, D, elem) && !kv_regs) {
     hipStream_t s = (hipStream_t)stream;
     if (ksrc > 0) {
@@ -1326,7 +1349,7 @@ mfa_status_t quantized_backward(const mfa_quantized_descriptor_t* desc,
       qsrc = 0;
     }
   }
-  return run_backward(p, elem, DP, ksrc, qsrc, phase, (hipStream_t)stream, kv_widen);
+  return run_backward(p, elem, DP, ksrc, qsrc, phase, (hipStream_t)stream, kv_widen, q_widen);
 }
 
 }  // namespace

@@ -87,6 +87,26 @@ __device__ __forceinline__ uint4 dequant_fast(const uint4 raw, float zp) {
       for (int k = 0; k < 4; ++k)
         w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
     }
+  } else if constexpr (E::prec == P_BF16) {
+    // BF16: q - zp in f32 (v_cvt_f32_ubyte of the biased byte, one subtract), then the two
+    // upper halves packed by one v_perm.  The host holds |zp| <= 128, so |q - zp| <= 256 has
+    // at most 8 significant bits: the f32 low halves are zero and the truncation is exact
+    // (the value f32_to_bf16 gives).
+    const float m = (SRC == SRC_I8 ? 128.0f : 8.0f) + zp;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float a, b;
+      if constexpr (SRC == SRC_I8) {
+        const uint32_t u = (k < 2 ? raw.x : raw.y) ^ 0x80808080u;
+        a = (float)((u >> (16 * (k & 1))) & 0xffu) - m;
+        b = (float)((u >> (16 * (k & 1) + 8)) & 0xffu) - m;
+      } else {
+        a = (float)((raw.x >> (8 * k)) & 15u) - m;
+        b = (float)((raw.x >> (8 * k + 4)) & 15u) - m;
+      }
+      w[k] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a),
+                                   0x07060302u);
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

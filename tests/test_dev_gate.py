@@ -18,7 +18,7 @@ KNOBS = {
     "MFA_FWD_STREAM_WGS": "7", "MFA_FWD_STREAM_SLOW": "1", "MFA_FWD_GEN": "1",
     "MFA_DISABLE_FAST": "1", "MFA_FWD2_TUNE": "1", "MFA_SHARE_XCD": "0", "MFA_SHARE_DV": "0",
     "MFA_SHARE_NT": "0", "MFA_SHARE_SWI": "0", "MFA_SHARE_IMG": "0", "MFA_KV8": "0",
-    "MFA_KV8_SLOTS": "2", "MFA_NO_DEQUANT_PASS": "1", "MFA_KV_REGS": "0", "MFA_DECODE": "0",
+    "MFA_BWDQ_BYTES": "1", "MFA_NO_DEQUANT_PASS": "1", "MFA_KV_REGS": "0", "MFA_DECODE": "0",
     "MFA_DECODE_MERGE": "1", "MFA_I8_BK": "1", "MFA_I8_SHARE": "0", "MFA_BWD256_BIGD": "1",
     "MFA_GEMM_IMG": "0", "MFA_GEMM_NN": "1", "MFA_GEMM3": "0",
 }

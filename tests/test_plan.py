@@ -61,7 +61,7 @@ def test_c5_forward_and_backward_phases():
     assert f["name"] == "mfa_fwd2_share_kernel<F16, 256, 32, false, false, false, false>"
     q = one(mfa.multihead_plan(d, K.backwardQuery))
     kv = one(mfa.multihead_plan(d, K.backwardKeyValue))
-    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32, false>"
+    assert q["name"] == "mfa_bwd_q_fast_kernel<F16, 256, 32, false, 0>"
     assert kv["name"] == "mfa_bwd_kv_fast_kernel<F16, 256, 32, 0, false>"
     assert q["workgroups"] == 32 * 8 * 32 and kv["workgroups"] == 32 * 8 * 32
     for r in (f, q, kv):
@@ -100,18 +100,32 @@ def test_quantized_plans():
     # Dequant-exact forward, FP16 Q + per-tensor INT8 K/V: one kernel widening the bytes as
     # it stages them (attention_fwd_kv8.hip), no pass.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
-    assert [r["name"] for r in mfa.quantized_plan(qx)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, 1, 3, 12, 14>"]
+    assert [r["name"] for r in mfa.quantized_plan(qx)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1>"]
     # backwardQuery: one dequantisation pass per quantised operand (kv_dequant.hip), then the
-    # tuned 16-bit kernel on the dense copies (K/V tiles stream through LDS).
-    assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardQuery)][2] == \
-        "mfa_bwd_q_fast_kernel<F16, 128, 64, false>"
+    # tuned 16-bit kernel on the dense copies (K/V tiles stream through LDS) ...
+    assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardQuery)] == \
+        ["mfa_kv_dequant_kernel<F16, 1>"] * 2 + ["mfa_bwd_q_fast_kernel<F16, 128, 64, false, 0>"]
+    # ... except with few query rows per kv head, where the pass does not pay: the same kernel
+    # stages the stored bytes through an LDS byte ring and widens them there (kv_bytes.h).
+    few = mfa.AttentionDescriptor.make(64, 8192, 128, low_precision=True, precision=P.FP16)
+    qf = mfa.quantized_descriptor(few, P.FP16, P.INT8, P.INT8, B=1, H=16)
+    assert [r["name"] for r in mfa.quantized_plan(qf, K.backwardQuery)] == \
+        ["mfa_bwd_q_fast_kernel<F16, 128, 64, false, 1>"]
     # backwardKeyValue reads each key block's K/V once into registers and widens them there:
     # the INT8 instantiation (SRC_I8 = 1), no pass.
     assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardKeyValue)] == \
         ["mfa_bwd_kv_fast_kernel<F16, 128, 64, 1, false>"]
     # INT4 K/V with an FP16 Q: the same on-load kernel (SRC_I4 = 2).
     q4h = mfa.quantized_descriptor(base, P.FP16, P.INT4, P.INT4, B=1, H=16)
-    assert [r["name"] for r in mfa.quantized_plan(q4h)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2, 1, 3, 12, 14>"]
+    assert [r["name"] for r in mfa.quantized_plan(q4h)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2>"]
+    # BF16 Q at the same shape, and FP16 Q at D = 256 (BASELINE configs[4]'s width): the
+    # same on-load kernel, no pass.
+    bb = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.BF16)
+    qb = mfa.quantized_descriptor(bb, P.BF16, P.INT8, P.INT8, B=1, H=16)
+    assert [r["name"] for r in mfa.quantized_plan(qb)] == ["mfa_fwd2_kv8_kernel<BF16, 128, 64, 1>"]
+    b256 = mfa.AttentionDescriptor.make(4096, 4096, 256, low_precision=True, precision=P.FP16)
+    q256 = mfa.quantized_descriptor(b256, P.FP16, P.INT8, P.INT8, B=2, H=32)
+    assert [r["name"] for r in mfa.quantized_plan(q256)] == ["mfa_fwd2_kv8_kernel<F16, 256, 32, 1>"]
     # A quantised Q takes the dequantisation pass for every operand.
     q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(q4)]

@@ -358,42 +358,71 @@ def test_dequant_pass_blockwise_and_quantized_query(gpu):
 
 
 @pytest.mark.parametrize("kv", [P.INT8, P.INT4])
-def test_dequant_pass_backward_on_fast_kernels(gpu, kv):
-    """Low-precision descriptor (FP16 Q and dO): after the pass the backward runs the tuned
-    kernels (plan checked) and matches the oracle on the dequantised values."""
-    B, H, S, D = 1, 2, 256, 128
-    rng = np.random.default_rng(23)
+@pytest.mark.parametrize("D,zps,S", [(128, (0, 0), 300), (64, (3, -1), 300), (256, (-2, 5), 300),
+                                     (128, (4, 2), 100)])
+def test_quantized_backward_on_fast_kernels(gpu, kv, D, zps, S, monkeypatch):
+    """Low-precision descriptor (FP16 Q and dO), per-tensor quantised K/V, causal: both phases
+    run the tuned kernels on the stored bytes — backwardQuery through its LDS byte ring
+    (forced with MFA_BWDQ_BYTES=1 at S = 300, the default below 128 query rows per kv head),
+    backwardKeyValue in registers — with no dequantisation pass (plan checked), match the
+    oracle on the dequantised values, and (S = 300) give dQ bit for bit as the pass + 16-bit
+    kernel path (the default there: the same kernel on the dense copy, the same MFMA
+    operands)."""
+    B, H = 1, 2
+    if S >= 128:
+        monkeypatch.setenv("MFA_BWDQ_BYTES", "1")
+    rng = np.random.default_rng(23 + D)
     Q, K, V, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) * 0.5 for _ in range(4))
-    kq, ks, kd = quantize_host(K, kv)
-    vq, vs, vd = quantize_host(V, kv)
+    lim = 120 if kv == P.INT8 else 8
+    kq8 = rng.integers(-lim, lim, (B, H, S, D)).astype(np.int8)
+    vq8 = rng.integers(-lim, lim, (B, H, S, D)).astype(np.int8)
+    ks, vs = 0.004 if kv == P.INT8 else 0.06, 0.005 if kv == P.INT8 else 0.07
+    kd = ((kq8.astype(np.float32) - zps[0]) * np.float32(ks)).astype(np.float32)
+    vd = ((vq8.astype(np.float32) - zps[1]) * np.float32(vs)).astype(np.float32)
+    if kv == P.INT8:
+        kt, vt = tdev(kq8.view(np.uint8), torch.uint8), tdev(vq8.view(np.uint8), torch.uint8)
+    else:  # nibble n encodes n - 8, element 2i in the low nibble (GEMMQuantization.swift:500-515)
+        pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
+        kt, vt = tdev(pack(kq8.astype(np.int32)), torch.uint8), tdev(pack(vq8.astype(np.int32)), torch.uint8)
     Qd, dOd = seen(Q, P.FP16), seen(dO, P.FP16)
     ref = ol.attention(Qd, kd, vd, dO=dOd, causal=True)
     base = mfa.AttentionDescriptor.make(S, S, D, causal=True, low_precision=True,
                                         precision=P.FP16)
     desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H)
-    kt, vt = tdev(kq, torch.uint8), tdev(vq, torch.uint8)
     tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
-    tk = mfa.quantized_tensor(kt, kv, scale=ks)
-    tv = mfa.quantized_tensor(vt, kv, scale=vs)
+    tk = mfa.quantized_tensor(kt, kv, scale=ks, zero_point=zps[0])
+    tv = mfa.quantized_tensor(vt, kv, scale=vs, zero_point=zps[1])
     o = tdev(ref["O"])
     l = torch.from_numpy(ref["L"]).half().to(DEV)
     do = to_device(dO, P.FP16)
-    dq = torch.empty((B, H, S, D), dtype=torch.float32, device=DEV)
-    dk, dv = torch.empty_like(dq), torch.empty_like(dq)
-    dvals = torch.empty((B, H, S), dtype=torch.bfloat16, device=DEV)
     qa = mfa.QuantizedAttention()
-    plan = (mfa.quantized_plan(desc, mfa.KernelType.backwardQuery, tq, tk, tv) +
-            mfa.quantized_plan(desc, mfa.KernelType.backwardKeyValue, tq, tk, tv))
-    assert plan[2]["name"].startswith("mfa_bwd_q_fast_kernel<F16, 128")
-    # backwardKeyValue widens the quantised K/V in the kernel's registers: no pass.
-    assert len(plan) == 4 and plan[3]["name"].startswith("mfa_bwd_kv_fast_kernel<F16, 128"), plan
-    mfa.last_launches()
-    qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
-    qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
-    torch.cuda.synchronize()
-    assert mfa.last_launches() == plan  # the log keeps the last four launches
+    src = 1 if kv == P.INT8 else 2
+
+    def run():
+        dq = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
+        dk, dv = torch.empty_like(dq), torch.empty_like(dq)
+        dvals = torch.empty((B, H, S), dtype=torch.bfloat16, device=DEV)
+        plan = (mfa.quantized_plan(desc, mfa.KernelType.backwardQuery, tq, tk, tv) +
+                mfa.quantized_plan(desc, mfa.KernelType.backwardKeyValue, tq, tk, tv))
+        mfa.last_launches()
+        qa.backwardQuery(desc, tq, tk, tv, o, do, l, dq, dvals)
+        qa.backwardKeyValue(desc, tq, tk, tv, do, l, dvals, dk, dv)
+        torch.cuda.synchronize()
+        assert mfa.last_launches() == plan[-4:]  # the log keeps the last four launches
+        return [r["name"] for r in plan], dq, dk, dv, dvals
+
+    names, dq, dk, dv, dvals = run()
+    assert names == [f"mfa_bwd_q_fast_kernel<F16, {D}, {32 if D == 256 else 64}, false, {src}>",
+                     f"mfa_bwd_kv_fast_kernel<F16, {D}, {32 if D == 256 else 64}, {src}, false>"], names
     for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
-        assert maxerr(t, ref[name]) < 5e-2, name
+        assert maxerr(t, ref[name]) < 5e-2 * max(1.0, np.abs(ref[name]).max()), name
+    if S < 128:
+        return
+    monkeypatch.delenv("MFA_BWDQ_BYTES")
+    names2, dq2, _, _, dvals2 = run()
+    assert names2[:2] == [f"mfa_kv_dequant_kernel<F16, {src}>"] * 2, names2
+    assert names2[2] == f"mfa_bwd_q_fast_kernel<F16, {D}, {32 if D == 256 else 64}, false, 0>", names2
+    assert torch.equal(dq, dq2) and torch.equal(dvals, dvals2)
 
 
 # ----------------------------------------------------------------------- integer matmul
@@ -601,28 +630,34 @@ def test_decode_nonzero_zero_point(gpu):
     assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
 
 
-# FP16 Q with per-tensor INT8 K/V at >= 128 query rows per kv head: the shared-tile kernel
-# widens the staged bytes to the integers q - zp inside its loop (attention_fwd_kv8.hip), with
-# the scales folded as in the dequantisation pass.  Held to the oracle on the dequantised
-# values and to the pass + 16-bit kernel path (MFA_KV8=0): bit-identical at D = 128, where the
-# two run the same tile loop on the same operands.
+# FP16 / BF16 Q with per-tensor INT8 / INT4 K/V at >= 128 query rows per kv head: the
+# shared-tile kernel widens the staged bytes to the integers q - zp inside its loop
+# (attention_fwd_kv8.hip), with the scales folded as in the dequantisation pass.  Held to the
+# oracle on the dequantised values and to the pass + 16-bit kernel path (MFA_KV8=0):
+# bit-identical at the padded widths D = 64, 128, 256, where the two run the same tile loop on
+# the same operands.
 @pytest.mark.parametrize("kv", [P.INT8, P.INT4])
-@pytest.mark.parametrize("B,H,Hkv,R,C,D,zps", [
-    (1, 4, 4, 300, 1000, 128, (0, 0)),    # odd block count: the last pair's group 1 idles
-    (2, 4, 2, 256, 333, 128, (0, 0)),     # GQA, partial last key tile
-    (1, 2, 2, 129, 4101, 96, (7, -5)),    # zero points, ragged rows and keys
-    (1, 8, 1, 512, 200, 112, (0, 3)),     # MQA
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,zps,qp", [
+    (1, 4, 4, 300, 1000, 128, (0, 0), P.FP16),    # odd block count: the last pair's group 1 idles
+    (2, 4, 2, 256, 333, 128, (0, 0), P.FP16),     # GQA, partial last key tile
+    (1, 2, 2, 129, 4101, 96, (7, -5), P.FP16),    # zero points, ragged rows and keys
+    (1, 8, 1, 512, 200, 112, (0, 3), P.FP16),     # MQA
+    (1, 4, 2, 300, 1000, 128, (3, -2), P.BF16),   # BF16 Q (f32 widening, exact truncation)
+    (1, 2, 2, 256, 777, 64, (0, 0), P.FP16),      # D 64: one 8-element chunk per thread
+    (1, 3, 3, 200, 300, 48, (5, 1), P.BF16),      # D 48 padded to 64
+    (1, 2, 2, 256, 1000, 256, (0, 0), P.FP16),    # D 256: bytes through the LDS byte ring
+    (2, 2, 1, 300, 333, 192, (-4, 6), P.BF16),    # D 192 padded to 256, MQA
 ])
-def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, monkeypatch):
+def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, qp, monkeypatch):
     rng = np.random.default_rng(R + C + D)
     Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
     lim = 120 if kv == P.INT8 else 8
     kq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
     vq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
     ks, vs = 0.015, 0.02
-    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=P.FP16)
-    desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H, Hkv=Hkv)
-    tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, qp), qp)
     if kv == P.INT8:
         kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
     else:  # nibble n encodes n - 8, element 2i in the low nibble (GEMMQuantization.swift:500-515)
@@ -631,11 +666,13 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, monkeypatch):
     tk = mfa.quantized_tensor(kt, kv, scale=ks, zero_point=zps[0])
     tv = mfa.quantized_tensor(vt, kv, scale=vs, zero_point=zps[1])
     src = 1 if kv == P.INT8 else 2
+    DP = 64 if D <= 64 else 128 if D <= 128 else 256
+    E = "F16" if qp == P.FP16 else "BF16"
     names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
     if kv == P.INT8 or D % 32 == 0:
-        assert names == [f"mfa_fwd2_kv8_kernel<F16, 128, 64, {src}, 1, 3, 12, 14>"], names
+        assert names == [f"mfa_fwd2_kv8_kernel<{E}, {DP}, {32 if DP == 256 else 64}, {src}>"], names
     else:  # INT4 rows of D / 2 bytes off 16-byte alignment: the dequantisation pass
-        assert names[0] == "mfa_kv_dequant_kernel<F16, 2>", names
+        assert names[0] == f"mfa_kv_dequant_kernel<{E}, 2>", names
 
     def run():
         o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
@@ -646,17 +683,19 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, monkeypatch):
 
     o1, l1 = run()
     monkeypatch.setenv("MFA_KV8", "0")
+    assert not mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)[-1]["name"].startswith(
+        "mfa_fwd2_kv8_kernel")
     o2, l2 = run()
     monkeypatch.delenv("MFA_KV8")
     kd = ((kq.astype(np.float32) - zps[0]) * np.float32(ks)).astype(np.float32)
     vd = ((vq.astype(np.float32) - zps[1]) * np.float32(vs)).astype(np.float32)
-    Qs = seen(Q, P.FP16)
+    Qs = seen(Q, qp)
     for h in sorted({0, H - 1}):
         ref = ol.attention(Qs[:, h:h + 1], kd[:, h % Hkv:h % Hkv + 1], vd[:, h % Hkv:h % Hkv + 1])
         assert maxerr(o1[:, h:h + 1], ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max()), h
         assert maxerr(l1[:, h:h + 1], ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max(), h
     assert np.isfinite(o1).all()
-    if D == 128:
+    if D == DP:
         assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
     else:
         assert maxerr(o1, o2) < 1e-5 and maxerr(l1, l2) < 2e-2
