@@ -33,6 +33,61 @@ __device__ __forceinline__ i16x8 widen_i8(uint32_t lo, uint32_t hi, float zp) {
   return __builtin_bit_cast(i16x8, dequant_fast<E, SRC_I8>(make_uint4(lo, hi, 0u, 0u), zp));
 }
 
+// 8 bytes holding nibble values n (0..15, from the INT4 V widening) -> 8 MFMA elements
+// n - zk4 (zk4 = zp + 8).  FP16: 0x64nn = 1024 + n by v_perm, no sign flip.
+template <class E>
+__device__ __forceinline__ i16x8 widen_u4(uint32_t lo, uint32_t hi, float zk4) {
+  if constexpr (E::prec == P_FP16) {
+    uint32_t w[4] = {__builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u),
+                     __builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u),
+                     __builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u),
+                     __builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u)};
+    const _Float16 m = (_Float16)(1024.0f + zk4);
+    const f16x2 mm = {m, m};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
+    return __builtin_bit_cast(i16x8, make_uint4(w[0], w[1], w[2], w[3]));
+  } else {
+    return widen_i8<E>(lo, hi, zk4);
+  }
+}
+
+// INT4 K fragments straight from the packed tile: 8 nibbles (n0 in the low nibble) -> 8 MFMA
+// elements n - 8 - zp (zk4 = zp + 8).  FP16: v_perm places the even nibbles n0 n2 n4 n6 and
+// the odd ones n1 n3 n5 n7 as the low bytes of 1024 + n (0x64nn) — one v_perm per pair, then a
+// packed subtract: the fragment holds the elements in the order kI4Perm, which the Q fragments
+// are loaded in too (the contraction over d does not care which lane slot holds which d, only
+// that Q and K agree).  BF16: natural order, f32 route as in mfa_stage.h dequant_fast.
+template <class E>
+__device__ __forceinline__ i16x8 nib_widen(uint32_t x, float zk4) {
+  if constexpr (E::prec == P_FP16) {
+    const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+    uint32_t w[4] = {__builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u),
+                     __builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u),
+                     __builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u),
+                     __builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u)};
+    const _Float16 m = (_Float16)(1024.0f + zk4);
+    const f16x2 mm = {m, m};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
+    return __builtin_bit_cast(i16x8, make_uint4(w[0], w[1], w[2], w[3]));
+  } else {
+    return __builtin_bit_cast(i16x8, dequant_fast<E, SRC_I4>(make_uint4(x, 0u, 0u, 0u), zk4 - 8.0f));
+  }
+}
+
+// Q fragment slot j holds element kI4Perm[j] of its 8-element group (FP16 INT4 K: the order
+// nib_widen produces).
+template <class E>
+__device__ __forceinline__ i16x8 i4_order(i16x8 v) {
+  if constexpr (E::prec == P_FP16)
+    return __builtin_shufflevector(v, v, 0, 2, 4, 6, 1, 3, 5, 7);
+  else
+    return v;
+}
+
 // Combines the np partials (m_s, l_s, O_s) of one query row for columns d .. d+3 and stores
 // O = Σ w_s O_s / (Σ w_s l_s + FLT_MIN), w_s = exp2(m_s - max m), and with write_l also
 // L = max m + log2 l.  Partial s is ml[s·mls] and the D floats at op + s·ops (global memory
@@ -70,15 +125,23 @@ __device__ __forceinline__ void merge_partials(const FwdParams& p, const float2*
   }
 }
 
+// s_waitcnt immediate for vmcnt(n) alone (n < 64: bits 3:0 and 15:14).
+constexpr int vm_wait(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+
 // SRC_I8: one byte per element.  SRC_I4: two per byte (element 2i in the low nibble,
-// GEMMQuantization.swift:500-515); the packed tile is staged by LDS-DMA as stored and widened
-// in LDS to the INT8 tile layout (nibble n as the byte n, the zero point raised by 8: the
-// nibble encodes n - 8), after which both paths run the same INT8 loop.
+// GEMMQuantization.swift:500-515), staged by LDS-DMA as stored.  K fragments are widened from
+// the packed tile in registers (nib_widen; each lane reads 16 consecutive elements = 8 bytes
+// for two k-steps, so the lane's k-step st covers d = 32·(st / 2) + 16·hh + 8·(st % 2) + j and
+// Q is loaded in that order; the packed K rows land XOR-swizzled by 16-byte chunk); the V tile
+// is widened in LDS to the INT8 tile layout (nibble n as the byte n, the zero point raised by
+// 8: the nibble encodes n - 8) and read by the INT8 loop's transposed reads.
 template <class E, int DP, int SRC = SRC_I8>
 __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(DecodeParams dp) {
   const FwdParams& p = dp.f;
   constexpr bool I4 = SRC == SRC_I4;
-  constexpr int BK = 32, NSLOT = 2, ND = DP / 32;
+  // INT4 keeps two tiles in flight (three ring slots in the INT8 ring's bytes: the packed
+  // tiles are half as large).
+  constexpr int BK = 32, NSLOT = SRC == SRC_I4 ? 3 : 2, ND = DP / 32;
   constexpr int ROWB = DP;                  // INT8 compute tile: one byte per element
   using T = Tile16<ROWB / 2>;               // [BK][ROWB bytes], 16-byte chunks XOR-swizzled
   constexpr int TILEB = BK * ROWB;          // one K or V compute tile
@@ -92,10 +155,12 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  // Per wave: NSLOT DMA slots (K at 2s·TILEBS, V after it); INT4 also one widened INT8 K and V
-  // tile after them (4·TILEB in all for INT8, 3·TILEB for INT4).
-  char* const ring = smem + wave * (NSLOT * 2 * TILEB);
-  char* const conv = ring + NSLOT * 2 * TILEBS;
+  // Per wave: NSLOT DMA slots (K at 2s·TILEBS, V after it); INT4 also the widened INT8 V tile
+  // after them (4·TILEB in all for both).
+  constexpr int WREG = NSLOT * 2 * TILEBS + (I4 ? TILEB : 0);
+  static_assert(WREG == 4 * TILEB, "per-wave LDS region");
+  char* const ring = smem + wave * WREG;
+  char* const conv = ring + NSLOT * 2 * TILEBS;  // INT4: the widened V tile
 
   const int split = blockIdx.x;
   const int u = blockIdx.y + gridDim.y * blockIdx.z;    // (b·H_kv + kvh)·nrt + rt
@@ -115,10 +180,10 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
         (const uint16_t*)p.q.ptr + (int64_t)b * p.q.sb + (int64_t)h * p.q.sh + (int64_t)q * p.q.ss;
 #pragma unroll
     for (int s = 0; s < DP / 16; ++s) {
-      const int d0 = 16 * s + 8 * hh;
+      const int d0 = I4 ? 32 * (s >> 1) + 16 * hh + 8 * (s & 1) : 16 * s + 8 * hh;
       i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (rvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-      qf[s] = v;
+      qf[s] = I4 ? i4_order<E>(v) : v;
     }
   }
 
@@ -136,13 +201,23 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   // layout.)
   constexpr int CPR = ROWBS / 16;
   constexpr int SH = I4 ? 1 : 0;  // element -> byte offsets
+  // Packed INT4 K rows: 16-byte chunk c of row r at physical chunk c ^ swz4(r), so the 8-byte
+  // fragment reads of a half-wave (32 rows, one chunk) spread over 16 slots (2-way at most).
+  auto swz4 = [](int r) {
+    if constexpr (CPR == 2) return (r >> 3) & 1;
+    else if constexpr (CPR == 4) return (r >> 2) & 3;
+    else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  };
   const int ssb = (int)(p.k.ss >> SH);
-  int poff[NPC];
+  int poff[NPC], voff[NPC];
 #pragma unroll
   for (int n = 0; n < NPC; ++n) {
     const int r = n * RP + lane / CPR;
-    const int ch = I4 ? lane % CPR : (lane % CPR) ^ T::swz(r);
+    const int ch = I4 ? (lane % CPR) ^ swz4(r) : (lane % CPR) ^ T::swz(r);
     poff[n] = ch * 16 < (p.D >> SH) ? r * ssb + ch * 16 : 0x40000000;
+    // V: INT8 as K; INT4 unswizzled (the LDS widening reads its rows in order).
+    const int cv = I4 ? lane % CPR : ch;
+    voff[n] = cv * 16 < (p.D >> SH) ? r * ssb + cv * 16 : 0x40000000;
   }
   const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> SH);
   const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> SH);
@@ -160,32 +235,32 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
     for (int n = 0; n < NPC; ++n) {
       const int rv = t * ssb;
       // V rows share the K piece geometry when the row strides agree (host-checked).
-      lds_dma16(vhead + rv, max(vbytes - rv, 0), poff[n], kdst + TILEBS + n * 1024);
+      lds_dma16(vhead + rv, max(vbytes - rv, 0), voff[n], kdst + TILEBS + n * 1024);
     }
   };
-  // INT4: the packed tile of this slot widened into the INT8 compute tiles (wave-private: the
-  // wave's own LDS accesses stay in order, no barrier).  Nibbles n0..n3 of a 16-bit half-word
-  // become the bytes n0..n3 by two shift-or-mask steps.
+  // INT4: the packed V tile of this slot widened into the INT8 compute tile (wave-private: the
+  // wave's own LDS accesses stay in order, no barrier).  A dword of 8 nibbles becomes the 8
+  // bytes n0..n7: the even and the odd nibbles masked out, then interleaved by two v_perm.
   auto widen_i4_tile = [&](int slot) {
     constexpr int NCP = ROWBS / 16, PER = BK * NCP / 64;
-    auto expand = [](uint32_t x) -> uint32_t {
-      x &= 0xFFFFu;
-      x = (x | (x << 8)) & 0x00FF00FFu;
-      return (x | (x << 4)) & 0x0F0F0F0Fu;
+    auto expand2 = [](uint32_t x, uint32_t& a, uint32_t& b) {
+      const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+      a = __builtin_amdgcn_perm(hi, lo, 0x05010400u);  // n0 n1 n2 n3
+      b = __builtin_amdgcn_perm(hi, lo, 0x07030602u);  // n4 n5 n6 n7
     };
+    const char* src = ring + slot * 2 * TILEBS + TILEBS;
+    char* dst = conv;
 #pragma unroll
-    for (int op = 0; op < 2; ++op) {
-      const char* src = ring + slot * 2 * TILEBS + op * TILEBS;
-      char* dst = conv + op * TILEB;
-#pragma unroll
-      for (int j = 0; j < PER; ++j) {
-        const int idx = lane + 64 * j, r = idx / NCP, pc = idx % NCP;
-        const uint4 w = *reinterpret_cast<const uint4*>(src + r * ROWBS + pc * 16);
-        *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc)) =
-            make_uint4(expand(w.x), expand(w.x >> 16), expand(w.y), expand(w.y >> 16));
-        *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc + 1)) =
-            make_uint4(expand(w.z), expand(w.z >> 16), expand(w.w), expand(w.w >> 16));
-      }
+    for (int j = 0; j < PER; ++j) {
+      const int idx = lane + 64 * j, r = idx / NCP, pc = idx % NCP;
+      const uint4 w = *reinterpret_cast<const uint4*>(src + r * ROWBS + pc * 16);
+      uint4 e0, e1;
+      expand2(w.x, e0.x, e0.y);
+      expand2(w.y, e0.z, e0.w);
+      expand2(w.z, e1.x, e1.y);
+      expand2(w.w, e1.z, e1.w);
+      *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc)) = e0;
+      *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc + 1)) = e1;
     }
   };
 
@@ -202,29 +277,44 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   float m = -kFltMax, lh = 0.f;
 
   if (mine > 0) issue(0, 0);
+  if (NSLOT == 3 && mine > 1) issue(1, 1);
   for (int i = 0; i < mine; ++i) {
-    const int slot = i & 1;
-    if (i + 1 < mine) {
-      issue(i + 1, slot ^ 1);
-      __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NPC));  // tile i landed, tile i+1 in flight
+    const int slot = i % NSLOT;
+    if (i + NSLOT - 1 < mine) {
+      issue(i + NSLOT - 1, (i + NSLOT - 1) % NSLOT);
+      __builtin_amdgcn_s_waitcnt(vm_wait((NSLOT - 1) * 2 * NPC));  // tile i landed
+    } else if (NSLOT == 3 && i + 1 < mine) {
+      __builtin_amdgcn_s_waitcnt(vm_wait(2 * NPC));  // tile i + 1 still in flight
     } else {
       wait_vm();
     }
     const char* kt = ring + slot * 2 * TILEB;
+    const char* vt = kt + TILEB;
     if constexpr (I4) {
       widen_i4_tile(slot);
-      kt = conv;
+      vt = conv;
     }
-    const char* vt = kt + TILEB;
     const int t = k0 + BK * (wave + 4 * i);
 
-    // S^T = K·Q^T: key l32 on the A operand's row, elements d = 16s + 8hh + j.
+    // S^T = K·Q^T: key l32 on the A operand's row, elements d = 16s + 8hh + j (INT4: the lane
+    // order above, two k-steps per 8-byte read of the packed row).
     f32x16 sa[1];
     sa[0] = zero16();
+    if constexpr (I4) {
+      const char* kp = ring + slot * 2 * TILEBS;
 #pragma unroll
-    for (int st = 0; st < DP / 16; ++st) {
-      const uint2 kb = *reinterpret_cast<const uint2*>(kt + T::off(l32, st) + 8 * hh);
-      sa[0] = E::mma(widen_i8<E>(kb.x, kb.y, zk), qf[st], sa[0]);
+      for (int a = 0; a < DP / 32; ++a) {
+        const uint2 kb =
+            *reinterpret_cast<const uint2*>(kp + l32 * ROWBS + 16 * (a ^ swz4(l32)) + 8 * hh);
+        sa[0] = E::mma(nib_widen<E>(kb.x, zk), qf[2 * a], sa[0]);
+        sa[0] = E::mma(nib_widen<E>(kb.y, zk), qf[2 * a + 1], sa[0]);
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < DP / 16; ++st) {
+        const uint2 kb = *reinterpret_cast<const uint2*>(kt + T::off(l32, st) + 8 * hh);
+        sa[0] = E::mma(widen_i8<E>(kb.x, kb.y, zk), qf[st], sa[0]);
+      }
     }
     if (t + BK > p.C) {
       // Keys past C: -inf (key offset acc_row(r, hh) within the tile).
@@ -267,7 +357,9 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
         const char* pa = vt + T::off(ks ? trow1 : trow0, col >> 4) + (col & 15);
         const i32x2d w = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
             (__attribute__((address_space(3))) i32x2d*)pa);
-        o[dt] = E::mma(widen_i8<E>((uint32_t)w[0], (uint32_t)w[1], zv), pb[ks], o[dt]);
+        o[dt] = E::mma(I4 ? widen_u4<E>((uint32_t)w[0], (uint32_t)w[1], zv)
+                          : widen_i8<E>((uint32_t)w[0], (uint32_t)w[1], zv),
+                       pb[ks], o[dt]);
       }
     }
   }
