@@ -23,6 +23,7 @@
 // Lazy rescaling (threshold 8 in log2 units, cdna_hip_programming.md T13) is kept: the running
 // max and the −m tile change only when a tile's max exceeds m + 8.
 #include "attention_fwd2.h"
+#include "kv_bytes.h"
 
 namespace mfa {
 
@@ -436,8 +437,42 @@ __global__ void __launch_bounds__(NWG * 128, 2) mfa_fwd2_pair_kernel(FwdParams p
 // LDS-DMA like the tiles (group 0 into the Q staging, group 1 into ring 1, unused before
 // phase 2) so that every prologue load is counted by hand — and step 0 waits for V0 between
 // its softmax and its PV.
-template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false>
-__global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
+// Quantised K/V staging of the shared-tile kernel (KVS != SRC_SAME): a thread's byte offset of
+// its chunk in a tile (out of range past D), one chunk's bytes of the tile at row t (rows past
+// the end read as zeros), and one chunk's widening into the 16-bit TileA image.
+template <int DP, int BK>
+__device__ __forceinline__ int share_byte_off(const Kv8Geo<DP, BK>& geo, int ss, int D, int sh) {
+  return geo.col < D ? geo.r * ss + (geo.col >> sh) : 0x40000000;
+}
+template <int CB>
+__device__ __forceinline__ uint4 share_ld_bytes(const char* head, int ss, int bytes, int t, int off) {
+  const int tb = t * ss;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(head + tb), (short)0, max(bytes - tb, 0), 0x00020000);
+  if constexpr (CB == 16) {
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    return make_uint4(a[0], a[1], a[2], a[3]);
+  } else {
+    const auto a = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+    return make_uint4(a[0], a[1], 0u, 0u);
+  }
+}
+template <class E, int DP, int KVS, int BK>
+__device__ __forceinline__ void share_widen2(char* img, const Kv8Geo<DP, BK>& geo, const uint4 raw,
+                                             float zp) {
+  widen_store<E, DP, KVS, 0>(img, geo.r, geo.ch0, raw, zp);
+  widen_store<E, DP, KVS, 1>(img, geo.r, geo.ch0 + 1, raw, zp);
+}
+
+// KVS: K/V storage — SRC_SAME (16-bit, LDS-DMA into the rings) or SRC_I8 / SRC_I4 per-tensor
+// quantised (mfa_fwd2_share_kv8_kernel): each step widens the next step's tile(s) from
+// registers into their 16-bit slots (the shared tile by all 512 threads, a group's own tile by
+// its 256) and loads the bytes of the step after it (attention_fwd_kv8.hip's scheme, in this
+// schedule), so the MFMA operands are those of the dequantisation pass + 16-bit kernel path.
+template <class E, int DP, int BK, bool MIRROR, bool NTS, bool IMG, bool DV, int KVS>
+__device__ __forceinline__ void fwd2_share_body(const FwdParams& p) {
+  constexpr bool QKV = KVS != SRC_SAME;
+  static_assert(!(QKV && DV), "quantised K/V: no deferred-V prologue");
   constexpr int NT = 256, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
   constexpr int QW = 32 * DP * 2;                    // one wave's 32 Q rows
@@ -475,12 +510,19 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
 
   DmaA<DP, BK, NT> kd, vd;         // a group's own tiles
   DmaA<DP, BK, 2 * NT> ksh, vsh;   // shared tiles, staged by all 8 waves
-  kd.init((int)p.k.ss * 2, p.C, p.D * 2, gt);
-  vd.init((int)p.v.ss * 2, p.C, p.D * 2, gt);
-  ksh.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
-  vsh.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
-  const char* khead = (const char*)p.k.ptr + ((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) * 2;
-  const char* vhead = (const char*)p.v.ptr + ((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) * 2;
+  constexpr int KSH = KVS == SRC_I4 ? 1 : 0;  // INT4: element -> byte offsets
+  auto head_of = [&](const Operand& op) {
+    const int64_t e = (int64_t)b * op.sb + (int64_t)kvh * op.sh;
+    return (const char*)op.ptr + (QKV ? e >> KSH : e * 2);
+  };
+  const char* khead = head_of(p.k);
+  const char* vhead = head_of(p.v);
+  if constexpr (!QKV) {
+    kd.init((int)p.k.ss * 2, p.C, p.D * 2, gt);
+    vd.init((int)p.v.ss * 2, p.C, p.D * 2, gt);
+    ksh.init((int)p.k.ss * 2, p.C, p.D * 2, tid);
+    vsh.init((int)p.v.ss * 2, p.C, p.D * 2, tid);
+  }
 
   // Adjacent pairs: an odd last block leaves group 1 without rows (it still stages tiles).
   const int rbA = MIRROR ? pi : 2 * pi;
@@ -559,6 +601,60 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     return s < S && i < nB;
   };
 
+  // QKV: the bytes of one step's tile(s) in registers — the shared tile's chunk of this thread
+  // (Kv8Geo over 512 threads), or two chunks of the group's own tile (over its 256 threads).
+  // Range-checked buffer loads: rows past C and chunks past D read as zeros (their widened
+  // values -zp meet masked keys, or Q / output columns past D).
+  using Geo = Kv8Geo<DP, BK>;
+  constexpr int CB = 16 >> KSH;  // stored bytes per 16-element chunk
+  uint4 rk0 = make_uint4(0u, 0u, 0u, 0u), rk1 = rk0, rv0 = rk0, rv1 = rk0;  // shared chunk in rk0 / rv0
+  // (a group tile: two chunks, 0 and 1)
+  const float zk = (float)p.k.zp, zv = (float)p.v.zp;
+  const int kss = QKV ? (int)(p.k.ss >> KSH) : 0, vss = QKV ? (int)(p.v.ss >> KSH) : 0;
+  const int kbytes = QKV ? (int)((int64_t)(p.C - 1) * kss + (p.D >> KSH)) : 0;
+  const int vbytes = QKV ? (int)((int64_t)(p.C - 1) * vss + (p.D >> KSH)) : 0;
+  const Geo gs(tid), g0(gt), g1(gt + 256);  // shared chunk; the group tile's two chunks
+  const int kos = share_byte_off(gs, kss, p.D, KSH), vos = share_byte_off(gs, vss, p.D, KSH);
+  const int ko0 = share_byte_off(g0, kss, p.D, KSH), vo0 = share_byte_off(g0, vss, p.D, KSH);
+  const int ko1 = share_byte_off(g1, kss, p.D, KSH), vo1 = share_byte_off(g1, vss, p.D, KSH);
+  // Staging, written out in place (closures holding references to these registers, or
+  // assignments to them under data-dependent branches, kept them in scratch).  Step s2's bytes:
+  // the shared tile's chunk (rk0 / rv0; the second loads read nothing) or the group tile's two
+  // chunks; a step without a tile for this group reads nothing (zero bytes in range).
+#define QKV_LOAD(S2)                                                                         \
+  do {                                                                                       \
+    int t_;                                                                                  \
+    const bool sh_ = (S2) < nA;                                                              \
+    const bool has_ = tile((S2), t_) || sh_;                                                 \
+    if (sh_) t_ = b0 + (S2) * BK;                                                            \
+    const int kb_ = has_ ? kbytes : 0, vb_ = has_ ? vbytes : 0;                              \
+    rk0 = share_ld_bytes<CB>(khead, kss, kb_, t_, sh_ ? kos : ko0);                          \
+    rv0 = share_ld_bytes<CB>(vhead, vss, vb_, t_, sh_ ? vos : vo0);                          \
+    rk1 = share_ld_bytes<CB>(khead, kss, sh_ ? 0 : kb_, t_, ko1);                            \
+    rv1 = share_ld_bytes<CB>(vhead, vss, sh_ ? 0 : vb_, t_, vo1);                            \
+  } while (0)
+  // Step s1's tile(s) from the registers into 16-bit slot SL of the shared or the group's ring.
+#define QKV_WIDEN(S1, SL)                                                                    \
+  do {                                                                                       \
+    int t_;                                                                                  \
+    const bool sh_ = (S1) < nA;                                                              \
+    if (sh_ || tile((S1), t_)) {                                                             \
+      char* const kd_ = (sh_ ? sk : kb0) + (SL) * TILEB;                                     \
+      char* const vd_ = (sh_ ? sv : vb0) + (SL) * TILEB;                                     \
+      const int r_ = sh_ ? gs.r : g0.r, c_ = sh_ ? gs.ch0 : g0.ch0;                          \
+      widen_store<E, DP, KVS, 0>(kd_, r_, c_, rk0, zk);                                      \
+      widen_store<E, DP, KVS, 1>(kd_, r_, c_ + 1, rk0, zk);                                  \
+      widen_store<E, DP, KVS, 0>(vd_, r_, c_, rv0, zv);                                      \
+      widen_store<E, DP, KVS, 1>(vd_, r_, c_ + 1, rv0, zv);                                  \
+      if (!sh_) {                                                                            \
+        widen_store<E, DP, KVS, 0>(kd_, g1.r, g1.ch0, rk1, zk);                              \
+        widen_store<E, DP, KVS, 1>(kd_, g1.r, g1.ch0 + 1, rk1, zk);                          \
+        widen_store<E, DP, KVS, 0>(vd_, g1.r, g1.ch0, rv1, zv);                              \
+        widen_store<E, DP, KVS, 1>(vd_, g1.r, g1.ch0 + 1, rv1, zv);                          \
+      }                                                                                      \
+    }                                                                                        \
+  } while (0)
+
   int q0 = (g == 0 && (nA > 0 || !MIRROR) ? rbA : rbB) * BQ;
   int qi = q0 + wg * 32 + l32;
   i16x8 qf[DP / 16];
@@ -580,6 +676,14 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
 #pragma unroll
     for (int ds = 0; ds < DP / 16; ++ds) qf[ds] = A::read_row_a(qdst, rbase, 0, ds);
     prescale_q2<E, DP>(qf, c);
+  } else if constexpr (QKV) {
+    // Bytes of step 0's tile(s), widened into slot 0; then step 1's bytes.
+    QKV_LOAD(0);
+    load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
+    QKV_WIDEN(0, 0);
+    QKV_LOAD(1);
+    prescale_q2<E, DP>(qf, c);
+    __syncthreads();
   } else {
     if (nA > 0) {
       ksh.issue(khead, b0, sk);
@@ -602,7 +706,12 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
     constexpr bool FIRST = decltype(first_c)::value;  // step 0 of the deferred-V prologue
     // Stage the next step's tile(s) into the slot read two steps ago.
     const int nx = (s + 1) & 1;
-    if (s + 1 < nA) {
+    if constexpr (QKV) {
+      // The next step's tile(s) widened from the bytes loaded a step ago; then the bytes of the
+      // step after it.
+      QKV_WIDEN(s + 1, nx);
+      QKV_LOAD(s + 2);
+    } else if (s + 1 < nA) {
       ksh.issue(khead, b0 + (s + 1) * BK, sk + nx * TILEB);
       vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
     } else {
@@ -712,10 +821,15 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
                              NoHook(), rlo, rhi);
       }
     }
-    if (sw && full_sw)
+    if constexpr (QKV) {
+      // Only the staging of B's Q rows (LDS-DMA, issued before step nA - 1) must land here;
+      // the byte loads stay in flight.
+      if (s == nA - 1) wait_vm();
+    } else if (sw && full_sw) {
       __builtin_amdgcn_s_waitcnt(0x0F70 | (NSW & 15) | ((NSW >> 4) << 14));
-    else
+    } else {
       wait_vm();
+    }
     __syncthreads();
   };
   MFA_STAMP(1);
@@ -827,6 +941,23 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
   MFA_STAMP(7);
 }
 
+#undef QKV_LOAD
+#undef QKV_WIDEN
+
+template <class E, int DP, int BK, bool MIRROR, bool NTS = false, bool IMG = false, bool DV = false>
+__global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kernel(FwdParams p) {
+  fwd2_share_body<E, DP, BK, MIRROR, NTS, IMG, DV, SRC_SAME>(p);
+}
+
+constexpr int DP_KV8 = 128;
+
+// Causal pairs with per-tensor INT8 / INT4 K/V widened on load (mirrored schedule, non-temporal
+// O image stores, A's O through the Q staging region at the switch; no deferred V).
+template <class E, int DP, int BK, int KVS>
+__global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kv8_kernel(FwdParams p) {
+  fwd2_share_body<E, DP, BK, true, true, true, false, KVS>(p);
+}
+
 template <class E, int DP, int BK, bool MIRROR = true>
 static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   // Adjacent pairs use ring 0 only (every step is shared, no merge).
@@ -899,6 +1030,36 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
   q.nblk = (p.R + NWG * 32 - 1) / (NWG * 32);
   const int npairs = (q.nblk + 1) / 2;
   return launch(kern, dim3(npairs * p.B * p.H), dim3(NWG * 128), LDS, stream, q);
+}
+
+// Causal per-tensor INT8 / INT4 K/V widened on load, in the mirrored shared-tile schedule
+// where fwd2_dispatch would run it for 16-bit operands (D = 128, causal only, at most ~1.5
+// rounds of the chip of blocks, or up to 3 for long rows); hipErrorNotSupported elsewhere
+// (the caller then takes the dequantisation pass).
+hipError_t fwd_share_kv8_dispatch(const FwdParams& p, int elem, int DP, int src,
+                                  hipStream_t stream) {
+  if (DP != 128 || !p.mask.causal || p.mask.window || p.mask.ranges || p.mask.amask)
+    return hipErrorNotSupported;
+  FwdParams q = p;
+  q.nblk = (p.R + 127) / 128;
+  const int blocks = q.nblk * p.B * p.H;
+  if (blocks > 768 && !(q.nblk >= 64 && blocks <= 1536)) return hipErrorNotSupported;
+  constexpr int BK = 64;
+  constexpr int RING = 8 * BK * DP_KV8 * 2 + 4 * 32 * DP_KV8 * 2;
+  constexpr int MERGE = 4 * (DP_KV8 / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4;
+  constexpr int OIMG = 128 * (DP_KV8 * 4 + 16);
+  constexpr int LDS = RING > MERGE ? (RING > OIMG ? RING : OIMG) : (MERGE > OIMG ? MERGE : OIMG);
+  static_assert(LDS <= 160 * 1024, "LDS");
+  const dim3 grid(((q.nblk + 1) / 2) * p.B * p.H);
+#define MFA_SKV8(ELEM, EE, SRC)                                                                   \
+  if (elem == ELEM && src == SRC)                                                                \
+    return launch(mfa_fwd2_share_kv8_kernel<EE, DP_KV8, BK, SRC>, grid, dim3(512), LDS, stream, q);
+  MFA_SKV8(P_FP16, F16, SRC_I8)
+  MFA_SKV8(P_FP16, F16, SRC_I4)
+  MFA_SKV8(P_BF16, BF16, SRC_I8)
+  MFA_SKV8(P_BF16, BF16, SRC_I4)
+#undef MFA_SKV8
+  return hipErrorNotSupported;
 }
 
 // hipErrorNotSupported when the configuration is not covered (the caller falls back).

@@ -733,8 +733,10 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
 
 // The on-load shared-tile forward (attention_fwd_kv8.hip): FP16 or BF16 Q (the compute type),
 // per-tensor INT8 or INT4 K/V (any zero point), D % 16 == 0 with D <= 256 (padded to 64, 128
-// or 256), no masks, dense rows with 16-byte aligned byte offsets.  MFA_KV8=0 routes these through the dequantisation pass
-// instead (A/B).
+// or 256), no masks, dense rows with 16-byte aligned byte offsets.  Causal at D = 128 runs the
+// mirrored shared-tile kernel's on-load instantiation where that schedule applies
+// (attention_fwd_v2.hip fwd_share_kv8_dispatch; the pass elsewhere).  MFA_KV8=0 routes these
+// through the dequantisation pass instead (A/B).
 bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int DP) {
   if (const char* e = mfa::dev_env("MFA_KV8")) {
     if (e[0] == '0') return false;
@@ -745,7 +747,8 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
   if (p.k.bscale || p.v.bscale) return false;
   if ((DP != 64 && DP != 128 && DP != 256) || p.D % 16 != 0 || !(p.c_log2 > 0.f)) return false;
   const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
-  if (p.mask.causal || p.mask.window || p.mask.amask || p.mask.ranges) return false;
+  if (p.mask.window || p.mask.amask || p.mask.ranges) return false;
+  if (p.mask.causal && DP != 128) return false;  // causal: the mirrored schedule at D = 128
   if (p.q.sd != 1 || !p.q.vec || p.o_sd != 1) return false;
   if (p.k.sd != 1 || p.v.sd != 1) return false;
   for (const mfa::Operand* o : {&p.k, &p.v})
@@ -878,9 +881,12 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     const hipError_t e = mfa::fwd_decode_dispatch(p, elem, ws, (hipStream_t)stream);
     if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (decode) launch");
   }
-  if (kv8_eligible(p, elem, qp, kp, vp, DP))
-    return hip_status(mfa::fwd_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream),
-                      "mfa_fwd (INT8 K/V on load) launch");
+  if (kv8_eligible(p, elem, qp, kp, vp, DP)) {
+    const hipError_t e =
+        p.mask.causal ? mfa::fwd_share_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream)
+                      : mfa::fwd_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream);
+    if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (INT8 K/V on load) launch");
+  }
   int kvsrc = src_kind(kp);
   if (dequant_pass_worth(R, H, Hkv, D, elem)) {
     hipStream_t s = (hipStream_t)stream;

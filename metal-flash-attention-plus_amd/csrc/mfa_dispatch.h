@@ -70,6 +70,8 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
 // FP16 Q with per-tensor INT8 / INT4 K/V (src SRC_I8 / SRC_I4) widened on load inside the
 // shared-tile loop (attention_fwd_kv8.hip); D <= 128 padded to 128, no masks.
 hipError_t fwd_kv8_dispatch(const FwdParams& p, int elem, int DP, int src, hipStream_t stream);
+hipError_t fwd_share_kv8_dispatch(const FwdParams& p, int elem, int DP, int src,
+                                  hipStream_t stream);
 // Causal 16-bit forward over equal key-tile ranges (attention_fwd_stream.hip): the workspace
 // it needs for p (0: p does not take it; the first *zero_bytes must be zero when allocated)
 // and the launch (p.ws set).

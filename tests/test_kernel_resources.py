@@ -23,7 +23,7 @@ HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd2_share_kernel", "mfa_
        "mfa_fwd_i8_kernel", "mfa_fwd2_kv8_kernel", "mfa_fwd_decode_kernel", "mfa_decode_merge",
        "mfa_bwd_q_fast_kernel", "mfa_bwd_kv_fast_kernel", "mfa_fwd_bigd_kernel",
        "mfa_bwd_q_bigd_kernel", "mfa_mla", "mfa_kv_dequant_kernel", "mfa_gemm2_kernel",
-       "mfa_gemm3_kernel", "qz_", "mfa_fwd_pipe_kernel")
+       "mfa_gemm3_kernel", "qz_", "mfa_fwd_pipe_kernel", "mfa_fwd2_share_kv8_kernel")
 # Known stack users, each a rare path, with a cap on what they may use (bytes of scratch per
 # lane, spilled VGPRs) so that growth is caught:
 # - the D > 256 backwardQuery with an FP32 dO (the quantised API's dO, DOS = SRC_F32ANY) keeps

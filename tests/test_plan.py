@@ -126,6 +126,11 @@ def test_quantized_plans():
     b256 = mfa.AttentionDescriptor.make(4096, 4096, 256, low_precision=True, precision=P.FP16)
     q256 = mfa.quantized_descriptor(b256, P.FP16, P.INT8, P.INT8, B=2, H=32)
     assert [r["name"] for r in mfa.quantized_plan(q256)] == ["mfa_fwd2_kv8_kernel<F16, 256, 32, 1>"]
+    # Causal INT8 at the C2 shape: the mirrored shared-tile kernel widening K/V on load.
+    c2 = mfa.AttentionDescriptor.make(4096, 4096, 128, causal=True, low_precision=True,
+                                      precision=P.FP16)
+    qc2 = mfa.quantized_descriptor(c2, P.FP16, P.INT8, P.INT8, B=1, H=16)
+    assert [r["name"] for r in mfa.quantized_plan(qc2)] == ["mfa_fwd2_share_kv8_kernel<F16, 128, 64, 1>"]
     # A quantised Q takes the dequantisation pass for every operand.
     q4 = mfa.quantized_descriptor(base, P.INT8, P.INT4, P.INT4, B=1, H=16)
     names = [r["name"] for r in mfa.quantized_plan(q4)]

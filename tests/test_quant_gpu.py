@@ -701,6 +701,68 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, qp, monkeypatch):
         assert maxerr(o1, o2) < 1e-5 and maxerr(l1, l2) < 2e-2
 
 
+# Causal, FP16 / BF16 Q with per-tensor INT8 / INT4 K/V where the 16-bit path runs the mirrored
+# shared-tile schedule (D = 128, up to ~1.5 rounds of blocks): the same schedule widening K/V on
+# load (attention_fwd_v2.hip mfa_fwd2_share_kv8_kernel).  Held to the oracle on the dequantised
+# values, and bit-identical to the pass + mirrored 16-bit kernel (MFA_KV8=0): phase-1 tiles
+# shared by both groups, phase-2 tiles per group, the switch and the merge all see the same
+# operands.
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("B,H,Hkv,R,C,zps,qp", [
+    (1, 4, 4, 1024, 1024, (0, 0), P.FP16),     # 8 blocks: 4 mirrored pairs
+    (1, 2, 2, 640, 640, (5, -3), P.FP16),      # 5 blocks: the middle block alone
+    (2, 4, 2, 1000, 1000, (0, 2), P.BF16),     # ragged rows, GQA
+    (1, 3, 1, 384, 1000, (-7, 0), P.FP16),     # more keys than rows, MQA
+    (1, 2, 2, 2048, 2048, (1, 1), P.BF16),
+])
+def test_kv8_causal_on_load(gpu, kv, B, H, Hkv, R, C, zps, qp, monkeypatch):
+    D = 128
+    rng = np.random.default_rng(R + 7 * C)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    lim = 120 if kv == P.INT8 else 8
+    kq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    vq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    ks, vs = 0.015, 0.02
+    base = mfa.AttentionDescriptor.make(R, C, D, causal=True, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, qp), qp)
+    if kv == P.INT8:
+        kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
+    else:
+        pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
+        kt, vt = tdev(pack(kq.astype(np.int32)), torch.uint8), tdev(pack(vq.astype(np.int32)), torch.uint8)
+    tk = mfa.quantized_tensor(kt, kv, scale=ks, zero_point=zps[0])
+    tv = mfa.quantized_tensor(vt, kv, scale=vs, zero_point=zps[1])
+    src = 1 if kv == P.INT8 else 2
+    E = "F16" if qp == P.FP16 else "BF16"
+    names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    assert names == [f"mfa_fwd2_share_kv8_kernel<{E}, 128, 64, {src}>"], names
+
+    def run():
+        o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
+        l = torch.full((B, H, R), float("nan"), dtype=torch.float16, device=DEV)
+        mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+        torch.cuda.synchronize()
+        return o.cpu().numpy(), l.float().cpu().numpy()
+
+    o1, l1 = run()
+    monkeypatch.setenv("MFA_KV8", "0")
+    names0 = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    assert names0[-1].startswith("mfa_fwd2_share_kernel<"), names0
+    o2, l2 = run()
+    monkeypatch.delenv("MFA_KV8")
+    kd = ((kq.astype(np.float32) - zps[0]) * np.float32(ks)).astype(np.float32)
+    vd = ((vq.astype(np.float32) - zps[1]) * np.float32(vs)).astype(np.float32)
+    Qs = seen(Q, qp)
+    for h in sorted({0, H - 1}):
+        ref = ol.attention(Qs[:, h:h + 1], kd[:, h % Hkv:h % Hkv + 1], vd[:, h % Hkv:h % Hkv + 1],
+                           causal=True)
+        assert maxerr(o1[:, h:h + 1], ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max()), h
+        assert maxerr(l1[:, h:h + 1], ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max(), h
+    assert np.isfinite(o1).all()
+    assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
+
+
 def _ref_dequant_transposed_block(e, B, H, S, D, bs, scales):
     """The reference's block lookup for a transposed quantised operand, written out per element
     (AttentionKernel+Accumulate.swift:461-472, AttentionKernel+OuterProduct.swift:301-316):

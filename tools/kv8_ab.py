@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the on-load quantised forward (attention_fwd_kv8.hip) against the dequantisation pass
+"""A/B of the on-load quantised forward (attention_fwd_kv8.hip; causal: the mirrored shared-tile
+kernel's on-load instantiation) against the dequantisation pass
 + 16-bit kernel path (MFA_KV8=0), per-tensor INT8 / INT4 K/V, at the C3 shape (FP16 and BF16
 Q), D = 64 and the C5 shape (D = 256).  Prints per-launch-sequence times from HIP events on one
 stream, best of 5 rounds, interleaved.  Development tool: python tools/kv8_ab.py"""
@@ -20,11 +21,15 @@ def main():
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream()
     g = torch.Generator(device=dev).manual_seed(3)
-    cases = [("C3 fp16", 1, 16, 8192, 128, P.FP16), ("C3 bf16", 1, 16, 8192, 128, P.BF16),
-             ("D64 fp16", 1, 32, 8192, 64, P.FP16), ("C5 fp16", 2, 32, 4096, 256, P.FP16),
-             ("C5 bf16", 2, 32, 4096, 256, P.BF16)]
+    cases = [("C3 fp16", 1, 16, 8192, 128, P.FP16, False), ("C3 bf16", 1, 16, 8192, 128, P.BF16, False),
+             ("D64 fp16", 1, 32, 8192, 64, P.FP16, False), ("C5 fp16", 2, 32, 4096, 256, P.FP16, False),
+             ("C5 bf16", 2, 32, 4096, 256, P.BF16, False),
+             ("C2c fp16", 1, 16, 4096, 128, P.FP16, True), ("C2c bf16", 1, 16, 4096, 128, P.BF16, True),
+             ("S8kc fp16", 1, 16, 8192, 128, P.FP16, True)]
+    if len(sys.argv) > 1:
+        cases = [c for c in cases if any(c[0].startswith(x) for x in sys.argv[1].split(","))]
     for kv in (P.INT8, P.INT4):
-        for name, B, H, S, D, qp in cases:
+        for name, B, H, S, D, qp, causal in cases:
             tdt = torch.float16 if qp == P.FP16 else torch.bfloat16
             q = ((torch.rand((B, H, S, D), generator=g, device=dev) * 2 - 1)).to(tdt)
             nb = D if kv == P.INT8 else D // 2
@@ -32,13 +37,14 @@ def main():
             v = torch.randint(0, 256, (B, H, S, nb), generator=g, device=dev, dtype=torch.uint8)
             o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
             l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
-            base = mfa.AttentionDescriptor.make(S, S, D, low_precision=True, precision=qp)
+            base = mfa.AttentionDescriptor.make(S, S, D, causal=causal, low_precision=True,
+                                                precision=qp)
             desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H)
             tq = mfa.quantized_tensor(q, qp)
             tk = mfa.quantized_tensor(k, kv, scale=0.01)
             tv = mfa.quantized_tensor(v, kv, scale=0.01)
             qa = mfa.QuantizedAttention()
-            fl = 4.0 * B * H * S * S * D
+            fl = 4.0 * B * H * S * S * D * (0.5 * (S + 1) / S if causal else 1.0)
 
             def run(onload):
                 if onload:
