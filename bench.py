@@ -209,6 +209,39 @@ def main():
         }
         del qf, kf, vf, o3, l3, kq, vq, kh, vh, k4, v4
 
+        # Causal INT8 K/V prefill at the C2 shape (dequant-exact, K/V widened on load in the
+        # mirrored shared-tile schedule), against the same forward on fp16 K/V.
+        S2 = args.seq
+        q2 = uniform((B, H, S2, D), torch.float16)
+        k2f = uniform((B, H, S2, D), torch.float32)
+        v2f = uniform((B, H, S2, D), torch.float32)
+        k2q, k2s, _, _ = mfa.quantize(k2f, mfa.Precision.INT8, rows=B * H * S2, cols=D)
+        v2q, v2s, _, _ = mfa.quantize(v2f, mfa.Precision.INT8, rows=B * H * S2, cols=D)
+        k2h, v2h = k2f.half(), v2f.half()
+        o2c = torch.empty((B, H, S2, D), dtype=torch.float32, device=dev)
+        l2c = torch.empty((B, H, S2), dtype=torch.float16, device=dev)
+        base2c = mfa.AttentionDescriptor.make(S2, S2, D, causal=True, low_precision=True,
+                                              precision=mfa.Precision.FP16)
+        qd2c = mfa.quantized_descriptor(base2c, mfa.Precision.FP16, mfa.Precision.INT8,
+                                        mfa.Precision.INT8, B=B, H=H)
+        tq2 = mfa.quantized_tensor(q2, mfa.Precision.FP16)
+        tk2 = mfa.quantized_tensor(k2q, mfa.Precision.INT8, scale=float(k2s.item()))
+        tv2 = mfa.quantized_tensor(v2q, mfa.Precision.INT8, scale=float(v2s.item()))
+        desc2c = mfa.MultiHeadDescriptor.make(base2c, B, H, S2, D)
+        ms_c8 = ev_time(lambda: qa.forward(qd2c, tq2, tk2, tv2, o2c, l2c, stream=stream))
+        ms_c16 = ev_time(lambda: mha.forward(desc2c, q2, k2h, v2h, o2c, l2c, stream=stream))
+        f2c = mfa.attention_flops(B, H, S2, S2, D, causal=True)
+        result["int8_causal"] = {
+            "workload": f"QuantizedAttention forward, INT8 K/V (per-tensor) + fp16 Q, B{B} H{H} "
+                        f"S{S2} D{D} causal (the C2 shape), dequant-exact",
+            "kernels": [r["name"] for r in mfa.quantized_plan(qd2c, mfa.KernelType.forward,
+                                                              tq2, tk2, tv2)],
+            "int8_tflops": round(f2c / (ms_c8 * 1e-3) / 1e12, 2),
+            "fp16_tflops_same_shape": round(f2c / (ms_c16 * 1e-3) / 1e12, 2),
+            "int8_ms": round(ms_c8, 4), "fp16_ms": round(ms_c16, 4),
+        }
+        del q2, k2f, v2f, k2q, v2q, k2h, v2h, o2c, l2c
+
         # INT8 K/V decode (the KV-cache shape INT8 K/V exists for): B32 H16, 8192 cached keys,
         # 1 and 16 query rows per head; HBM-bound on the INT8 K/V read (2·D bytes per key).
         Bd, Hd, Cd, Dd = 32, 16, 8192, 128
