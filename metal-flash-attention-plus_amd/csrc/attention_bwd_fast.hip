@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     constexpr bool late_dma = MSK && DP >= 256;
     auto issue_next = [&]() {
       if (MSK && has_next) am_issue(hn, tn, am0 + (cur ^ 1) * BQ * BK);
-      if (!spread_dma<DP>() && has_next) {
+      if (!(spread_dma<DP>() && !MSK) && has_next) {
         qd.issue(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB);
         od.issue(ohead(hn), tn, ob0 + (cur ^ 1) * TILEB);
       }
@@ -762,7 +762,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     auto dma_hook = [&](int i) {
       constexpr int PPW = DmaA<DP, BQ, NT>::PPW;
       constexpr int EVERY = MFA_SPREAD_EVERY;
-      if (spread_dma<DP>() && (i % EVERY) == 0 && i / EVERY < 2 * PPW && has_next) {
+      if (spread_dma<DP>() && !MSK && (i % EVERY) == 0 && i / EVERY < 2 * PPW && has_next) {
         const int k = i / EVERY;
         if (k < PPW)
           qd.issue_piece(qhead(hn), tn, qb0 + (cur ^ 1) * TILEB, k);
@@ -855,7 +855,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       // No row of this step sees the key block: nothing to add (the next tiles' DMA still
       // lands before the barrier).
       if (late_dma) issue_next();
-      static_assert(!MSK || !spread_dma<DP>(), "mask steps issue the next tiles up front");
+      // (Mask steps issue the next tiles up front: no spread pieces under MSK.)
     } else if constexpr (DP <= 128) {
       // S = Q·K^T; masks; dP = dO·V^T with P = exp2(S·c − L) computed between its MFMAs;
       // dV^T += dO^T·P with dS = P∘(dP·scale − D) computed between its MFMAs; dK^T += Q^T·dS.
