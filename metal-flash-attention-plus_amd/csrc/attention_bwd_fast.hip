@@ -533,8 +533,15 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   int2* const rg0 = reinterpret_cast<int2*>(db0 + 2 * BQ);
   float* const am0 = reinterpret_cast<float*>(rg0 + 2 * BQ);
   int* const fl0 = reinterpret_cast<int*>(am0 + 2 * BQ * 128);
+  // MSK without an additive mask: the mask tile region holds every row's interval (rgall, up
+  // to RCAP rows) and every query tile's step flags (flall), computed once in the pre-pass, so
+  // the steps neither load ranges nor wait on wave 0 to convert them.
+  constexpr int AMB = 2 * BQ * 128 * 4, RCAP = (AMB - 512) / 8;
+  int2* const rgall = reinterpret_cast<int2*>(am0);
+  uint8_t* const flall = reinterpret_cast<uint8_t*>(rgall + RCAP);
 
   const int tid = threadIdx.x;
+  BST_DECL();  // (diagnostic builds: slot 7 = everything before the step loop)
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
@@ -546,8 +553,11 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
   const int ki = k0 + wave * 32 + l32;
   const bool kvalid = ki < p.C;
 
+  // The key block's K and V rows (MFMA A operands for the whole kernel).  Under MSK they are
+  // issued right after the pre-pass's range loads, so those do not wait behind them (vmcnt
+  // counts in issue order) while their latencies still overlap.
   i16x8 kf[DS], vf[DS];
-  {
+  auto load_kv = [&]() __attribute__((always_inline)) {
     const int kk = kvalid ? ki : 0;
     if constexpr (KVQ != SRC_SAME) {
       // Quantised per-tensor K/V (QuantizedAttention.backwardKeyValue): the key block's rows
@@ -573,36 +583,54 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       load_frags16<DP>(vf, (const uint16_t*)p.v.ptr + (int64_t)b * p.v.sb +
                                (int64_t)kvh * p.v.sh + (int64_t)kk * p.v.ss, kvalid, p.D, hh);
     }
-  }
-
+  };
+  if constexpr (!MSK) load_kv();
   int qbeg = 0, qend = p.R;
   if (p.mask.causal && p.mask.skip_ok) qbeg = (k0 / BQ) * BQ;
   if (p.mask.window && p.mask.skip_ok) {
     const int64_t hi = (int64_t)k0 + BK + (int64_t)p.mask.window_size;
     if (hi < qend) qend = (int)hi;
   }
+  const bool pre = MSK && !p.mask.amask && p.R <= RCAP;
   if constexpr (MSK) {
     // The rows that see this key block (their unmasked interval meets [k0, k0 + BK)) or sit at
     // the mask level (no unmasked key: they see every key): the query tiles run from the first
     // to the last of them only (the intervals are the same for every head of the kv group).
     // A pre-pass over the rows' intervals, one row per thread per 256.
+    // (32-bit: C and R are below 2^31 and range ends are clamped to C; 16 rows per thread in
+    // flight at once — at R = 4096 every thread's rows take one load latency.)
     int rmin = p.R, rmax = -1;
-#pragma unroll 8
-    for (int q = tid; q < p.R; q += NT) {
-      int64_t lo = 0, hi = p.C;
-      if (p.mask.ranges) {
-        const uint2 r = *reinterpret_cast<const uint2*>(
-            p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + q));
-        lo = r.x;
-        hi = min((int64_t)r.y, (int64_t)p.C);
+    const uint2* rrow = reinterpret_cast<const uint2*>(p.mask.ranges) + (int64_t)(b * p.Hkv + kvh) * p.R;
+    const int ws = (int)min(p.mask.window_size, 0x7fffffffu);
+    constexpr int PRE_N = 16;  // rows per thread whose loads are in flight together
+    // The first chunk runs on every thread (its loads guarded), so every lane issues load_kv.
+    int q0 = tid;
+    do {
+      uint2 rr[PRE_N];
+#pragma unroll
+      for (int j = 0; j < PRE_N; ++j) {
+        const int q = q0 + j * NT;
+        rr[j] = make_uint2(0u, 0x7fffffffu);
+        if (p.mask.ranges && q < p.R) rr[j] = rrow[q];
       }
-      if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
-      if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
-      if (lo >= hi || (lo < k0 + BK && hi > k0)) {
-        rmin = min(rmin, q);
-        rmax = max(rmax, q);
+      if (q0 == tid) load_kv();
+#pragma unroll
+      for (int j = 0; j < PRE_N; ++j) {
+        const int q = q0 + j * NT;
+        if (q < p.R) {
+          int lo = (int)min(rr[j].x, 0x7fffffffu);
+          int hi = (int)min(rr[j].y, (uint32_t)p.C);
+          if (p.mask.causal) hi = min(hi, q + 1);
+          if (p.mask.window) lo = max(lo, q - ws);
+          if (lo >= hi || (lo < k0 + BK && hi > k0)) {
+            rmin = min(rmin, q);
+            rmax = max(rmax, q);
+          }
+          if (pre) rgall[q] = lo >= hi ? make_int2(p.C, 0) : make_int2(lo, hi);
+        }
       }
-    }
+      q0 += PRE_N * NT;
+    } while (q0 < p.R);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       rmin = min(rmin, __shfl_xor(rmin, o));
@@ -619,6 +647,20 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     __syncthreads();
     qbeg = max(qbeg, (rmin / BQ) * BQ);
     qend = min(qend, rmax + 1);
+    if (pre) {
+      // Step flags of the query tiles [qbeg, qend), one wave per tile (lane = row); the barrier
+      // before the loop orders them for every wave.
+      for (int i = qbeg / BQ + wave; i * BQ < qend; i += NT / 64) {
+        const int q = i * BQ + lane;
+        const bool v = lane < BQ && q < p.R;
+        const int2 e = v ? rgall[q] : make_int2(0, 0);
+        const bool empty = e.x >= e.y;
+        const bool skip = !v || (!empty && (e.y <= k0 || e.x >= k0 + BK));
+        const bool full = !v || (!empty && e.x <= k0 && e.y >= min(k0 + BK, p.C));
+        const int f = (__ballot(skip) == ~0ull ? 1 : 0) | (__ballot(full) == ~0ull ? 2 : 0);
+        if (lane == 0) flall[i] = (uint8_t)f;
+      }
+    }
   }
   const int ntile = qbeg < qend ? (qend - qbeg + BQ - 1) / BQ : 0;
   const int ngroup = (p.H - kvh + p.Hkv - 1) / p.Hkv;  // query heads h = kvh + g*Hkv
@@ -649,7 +691,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
                      : reinterpret_cast<const uint32_t*>(p.l)[r];
       draw = p.d_bf16 ? (uint32_t)reinterpret_cast<const uint16_t*>(p.dD)[r]
                       : reinterpret_cast<const uint32_t*>(p.dD)[r];
-      if (MSK && p.mask.ranges)  // ranges are per kv head: [B, H_kv, R, 2]
+      if (MSK && p.mask.ranges && !pre)  // ranges are per kv head: [B, H_kv, R, 2]
         rraw = *reinterpret_cast<const uint2*>(
             p.mask.ranges + 2 * ((int64_t)(b * p.Hkv + kvh) * p.R + (ldv ? q : 0)));
     }
@@ -665,15 +707,17 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       const float dv = p.d_bf16 ? bf16_to_f32((uint16_t)draw) : __builtin_bit_cast(float, draw);
       lb0[buf * BQ + tid] = ldv ? lv : __builtin_inff();
       db0[buf * BQ + tid] = ldv ? dv : 0.f;
-      if constexpr (MSK) {
+      if (MSK && !pre) {
+        // 32-bit: C and R are below 2^31, and range ends are clamped to C.
         const int q = tq + tid;
-        int64_t lo = 0, hi = p.C;
+        int lo = 0, hi = p.C;
         if (p.mask.ranges) {
-          lo = rraw.x;
-          hi = min((int64_t)rraw.y, (int64_t)p.C);
+          lo = (int)min(rraw.x, 0x7fffffffu);
+          hi = (int)min(rraw.y, (uint32_t)p.C);
         }
-        if (p.mask.causal) hi = min(hi, (int64_t)q + 1);
-        if (p.mask.window) lo = max(lo, (int64_t)q - (int64_t)p.mask.window_size);
+        if (p.mask.causal) hi = min(hi, q + 1);
+        if (p.mask.window)
+          lo = max(lo, q - (int)min(p.mask.window_size, 0x7fffffffu));
         const bool empty = lo >= hi;
         const int elo = empty ? p.C : (int)lo, ehi = empty ? 0 : (int)hi;
         rg0[buf * BQ + tid] = make_int2(elo, ehi);
@@ -706,16 +750,17 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     }
   };
 
-  BST_DECL();
   f32x16 dk[ND], dv[ND];
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
   const float c = p.c_log2, sc = p.scale;
   const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
-  // P = exp2(S·c − L); MSK: rows at the mask level take the rounded product first.
+  // P = exp2(S·c − L).  MSK takes the rounded product first for every row (two VALU, no
+  // per-lane select, as the query phase does): exact for rows at the mask level, within
+  // rounding of the fused form elsewhere.
   auto pexp = [&](float x, float l) {
     if constexpr (MSK)
-      return __builtin_amdgcn_exp2f(l < kMaskLevel ? mul_rn(x, c) - l : __builtin_fmaf(x, c, -l));
+      return __builtin_amdgcn_exp2f(mul_rn(x, c) - l);
     else
       return __builtin_amdgcn_exp2f(__builtin_fmaf(x, c, -l));
   };
@@ -774,9 +819,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     const char* ot = ob0 + cur * TILEB;
     const float* lt = lb0 + cur * BQ;
     const float* dtl = db0 + cur * BQ;
-    const int2* rgt = rg0 + cur * BQ;
+    const int2* rgt = pre ? rgall + t : rg0 + cur * BQ;
     const float* amt = am0 + cur * BQ * BK;  // + this lane's key column (at the reads)
-    const int flags = MSK ? __builtin_amdgcn_readfirstlane(fl0[cur]) : 0;
+    const int flags = MSK ? __builtin_amdgcn_readfirstlane(pre ? (int)flall[t / BQ] : fl0[cur]) : 0;
 
     f32x16 s[NJ], dp[NJ];
 #pragma unroll

@@ -1,6 +1,8 @@
 // bwd_stamps.hip — diagnostic build of the fast backward with per-wave phase cycle totals of
 // backwardKeyValue (development tool; not part of libmfa_amd.so).  Build: make -C tools/diag
-// Run: tools/diag/bwd_stamps [B] [H] [S] [D]   (fp16, non-causal)
+// Run: tools/diag/bwd_stamps [B] [H] [S] [D] [band]   (fp16, non-causal; band > 0: sparse
+// ranges of `band` 128-key blocks per 128-row block, as bench.py's buildBlockSparse row, which
+// runs the mask instantiation)
 #define MFA_BSTAMPS 1
 #include "../../metal-flash-attention-plus_amd/csrc/attention_bwd_fast.hip"
 
@@ -36,6 +38,7 @@ int main(int argc, char** argv) {
   const int H = argc > 2 ? atoi(argv[2]) : 32;
   const int S = argc > 3 ? atoi(argv[3]) : 4096;
   const int D = argc > 4 ? atoi(argv[4]) : 128;
+  const int band = argc > 5 ? atoi(argv[5]) : 0;
   const size_t n = (size_t)B * H * S * D;
   uint16_t *q, *k, *v, *dO;
   float *l, *dd, *o, *dq, *dk, *dv;
@@ -61,6 +64,22 @@ int main(int argc, char** argv) {
   p.B = B; p.H = H; p.Hkv = H; p.R = S; p.C = S; p.D = D; p.group = 1;
   const float scale = 1.f / sqrtf((float)D);
   p.c_log2 = 1.442695041f * scale; p.scale = scale; p.dscale = scale; p.dq_mul = 1.f; p.dk_mul = 1.f;
+  if (band > 0) {
+    // Row q of every head keeps keys [128·c0, 128·(c0 + band)) with c0 centred on its block.
+    const int nb = S / 128;
+    std::vector<uint32_t> rg((size_t)B * H * S * 2);
+    for (int bh = 0; bh < B * H; ++bh)
+      for (int q = 0; q < S; ++q) {
+        const int i = q / 128;
+        const int c0 = std::min(std::max(0, i - band / 2), nb - band);
+        rg[((size_t)bh * S + q) * 2] = 128u * c0;
+        rg[((size_t)bh * S + q) * 2 + 1] = 128u * (c0 + band);
+      }
+    uint32_t* drg;
+    CK(hipMalloc(&drg, rg.size() * 4));
+    CK(hipMemcpy(drg, rg.data(), rg.size() * 4, hipMemcpyHostToDevice));
+    p.mask.ranges = drg;
+  }
   hipStream_t st;
   CK(hipStreamCreate(&st));
   hipEvent_t e0, e1;
@@ -91,8 +110,9 @@ int main(int argc, char** argv) {
   }
   double all = 0;
   for (int s = 0; s < 8; ++s) all += tot[s];
-  const int nsteps = S / (D >= 256 ? 32 : 64);
-  printf("waves %d; per wave per step (shader cycles):\n", nw);
+  const int nsteps = band > 0 ? 1 : S / (D >= 256 ? 32 : 64);
+  printf("waves %d; per wave %s (shader cycles); per-wave total %.0f cycles:\n", nw,
+         band > 0 ? "in all" : "per step", all / nw);
   for (int s = 0; s < 8; ++s)
     printf("  %-14s %8.0f  (%.1f%%)\n", names[s], tot[s] / nw / (s == 7 ? 1 : nsteps), 100.0 * tot[s] / all);
   return 0;
