@@ -77,10 +77,13 @@ __device__ __forceinline__ uint4 dequant_fast(const uint4 raw, float zp) {
       for (int k = 0; k < 4; ++k)
         w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
     } else {  // INT4 nibble n encodes n - 8
-      const uint32_t x = raw.x;
+      // Even elements (low nibbles) and odd ones (high nibbles) masked out once, then each
+      // pair's two bytes placed as the low bytes of its halfwords by one v_perm (0x0C selects
+      // a zero byte) and the 0x64 exponent bytes OR-ed in: 15 VALU per 8 elements, not 20.
+      const uint32_t lo = raw.x & 0x0F0F0F0Fu, hi = (raw.x >> 4) & 0x0F0F0F0Fu;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        w[k] = 0x64006400u | ((x >> (8 * k)) & 0xFu) | (((x >> (8 * k + 4)) & 0xFu) << 16);
+        w[k] = __builtin_amdgcn_perm(hi, lo, 0x0C040C00u + 0x00010001u * k) | 0x64006400u;
       const _Float16 m = (_Float16)(1032.0f + zp);
       const f16x2 mm = {m, m};
 #pragma unroll
