@@ -173,6 +173,9 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   const int row = rt * 32 + l32;
   const bool rvalid = row < dp.rows;
   i16x8 qf[DP / 16];
+  // Causal: the lane's query index sees keys 0 .. qcol (the host caps C at R, past which no
+  // row sees a key).
+  const int qcol = rvalid ? row % p.R : 0x3fffffff;
   {
     const int g = rvalid ? row / p.R : 0, q = rvalid ? row % p.R : 0;
     const int h = kvh + g * p.Hkv;
@@ -316,9 +319,11 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
         sa[0] = E::mma(widen_i8<E>(kb.x, kb.y, zk), qf[st], sa[0]);
       }
     }
-    if (t + BK > p.C) {
-      // Keys past C: -inf (key offset acc_row(r, hh) within the tile).
-      mask_outside<1>(sa, -0x40000000, p.C - t - 4 * hh - 1, -__builtin_inff());
+    if (t + BK > p.C || (p.mask.causal && t + BK - 1 > qcol)) {
+      // Keys past C, and (causal) keys past the lane's query index: -inf (key offset
+      // acc_row(r, hh) within the tile).
+      const int last = p.mask.causal ? min(p.C - 1, qcol) : p.C - 1;
+      mask_outside<1>(sa, -0x40000000, last - t - 4 * hh, -__builtin_inff());
     }
     f32x16& s = sa[0];
     float mx = s[0];
@@ -431,6 +436,9 @@ __global__ void __launch_bounds__(256) mfa_decode_merge_kernel(DecodeParams dp) 
                  4 * lane, lane == 0);
 }
 
+// Keys a decode call reads: all C, or under a causal mask only those some query row sees.
+int decode_keys(int R, int C, bool causal) { return causal ? (C < R ? C : R) : C; }
+
 // Split of the key range: enough workgroups for two per CU (512) when the units alone do not
 // provide them, each wave at least 4 tiles (128 keys).
 void decode_layout(int B, int Hkv, int rows, int C, int* nrt, int* nsplit, int* chunk) {
@@ -466,8 +474,10 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
     return hipErrorNotSupported;
   DecodeParams dp;
   dp.f = p;
+  // Causal (key <= query index): no row sees a key past R - 1.
+  if (p.mask.causal) dp.f.C = decode_keys(p.R, p.C, true);
   dp.rows = (p.H / p.Hkv) * p.R;
-  decode_layout(p.B, p.Hkv, dp.rows, p.C, &dp.nrt, &dp.nsplit, &dp.chunk);
+  decode_layout(p.B, p.Hkv, dp.rows, dp.f.C, &dp.nrt, &dp.nsplit, &dp.chunk);
   const size_t parts = (size_t)p.B * p.Hkv * dp.nrt * dp.nsplit * 4 * 32;
   dp.opart = (float*)workspace;
   dp.mlpart = workspace ? (float2*)((char*)workspace + ((parts * p.D * 4 + 255) & ~(size_t)255))

@@ -710,7 +710,7 @@ bool i8mma_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
 
 // The split-KV decode kernel (attention_decode.hip): FP16/BF16 Q, per-tensor INT8 or INT4
 // K/V with the same row layout, 16-byte rows (INT4: D % 32 == 0, 16-byte packed rows), D <= 256,
-// no mask, dense O rows.
+// no mask but causal, dense O rows.
 bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) {
   if (const char* e = mfa::dev_env("MFA_DECODE")) {
     if (e[0] == '0') return false;
@@ -721,7 +721,8 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
   const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
   if (p.k.bscale || p.v.bscale) return false;
   if (p.D % (16 << sh) != 0 || p.D > 256 || p.C <= 0 || !(p.c_log2 > 0.f)) return false;
-  if (p.mask.causal || p.mask.window || p.mask.amask || p.mask.ranges) return false;
+  // Causal: key <= query index, masked per lane in the kernel; keys past R are never read.
+  if (p.mask.window || p.mask.amask || p.mask.ranges) return false;
   if (p.q.sd != 1 || !p.q.vec || p.k.sd != 1 || p.v.sd != 1) return false;
   const int64_t al = 16 << sh;
   if (p.k.ss != p.v.ss || p.k.ss % al || p.k.sh % al || p.k.sb % al || p.v.sh % al ||
@@ -872,7 +873,8 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     // The split-KV partials workspace (scratch slot 9), unless one split per unit merges in
     // LDS (decode_workspace_bytes returns 0: nothing is allocated).
     void* ws = nullptr;
-    const size_t wsb = mfa::decode_workspace_bytes(B, Hkv, (H / Hkv) * R, C, D);
+    const size_t wsb = mfa::decode_workspace_bytes(B, Hkv, (H / Hkv) * R,
+                                                   mfa::decode_keys(R, C, p.mask.causal), D);
     if (wsb && mfa::plan_capture()) {
       ws = (void*)kPlanDummy;
     } else if (wsb && (st = scratch(wsb, &ws, 9, (hipStream_t)stream)) != MFA_SUCCESS) {

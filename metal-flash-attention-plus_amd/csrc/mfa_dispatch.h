@@ -66,6 +66,7 @@ hipError_t bwd_bigd_dispatch(const BwdParams& p, int kind, int elem, hipStream_t
 // Split-KV decode forward for per-tensor INT8 K/V (attention_decode.hip) and the workspace it
 // needs (partials of every wave).
 size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D);
+int decode_keys(int R, int C, bool causal);
 hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hipStream_t stream);
 // FP16 Q with per-tensor INT8 / INT4 K/V (src SRC_I8 / SRC_I4) widened on load inside the
 // shared-tile loop (attention_fwd_kv8.hip); D <= 128 padded to 128, no masks.

@@ -549,6 +549,35 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
         assert torch.equal(o, o3) and torch.equal(l, l3)
 
 
+# Causal masks on the split-KV decode kernel (key <= query index, masked per lane; the host
+# reads no key past R - 1): INT8 and INT4, FP16 / BF16 Q, GQA, against the oracle and the
+# generic dequant-on-load kernel (MFA_DECODE=0).
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,qp", [
+    (2, 4, 4, 16, 1000, 128, P.FP16),   # 16 rows: keys 0..15 at most
+    (1, 8, 2, 3, 777, 64, P.BF16),      # GQA: 12 rows per kv head
+    (1, 16, 1, 4, 300, 128, P.FP16),    # MQA, two row tiles
+    (1, 2, 2, 100, 90, 256, P.BF16),    # C < R: every key seen by the last rows
+])
+def test_decode_causal(gpu, kv, B, H, Hkv, R, C, D, qp, monkeypatch):
+    rng = np.random.default_rng(R * 31 + C)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
+    base = mfa.AttentionDescriptor.make(R, C, D, causal=True, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
+    names = [r["name"] for r in mfa.quantized_plan(desc)]
+    assert names[0].startswith("mfa_fwd_decode_kernel<"), names
+    o, l, deq, _ = run_qforward(Q, K, V, qp, kv, kv, causal=True)
+    ref = ol.attention(deq["Q"], deq["K"], deq["V"], causal=True)
+    assert np.isfinite(o.cpu().numpy()).all()
+    assert maxerr(o, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
+    assert maxerr(l, ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max()
+    monkeypatch.setenv("MFA_DECODE", "0")
+    o2, _, _, _ = run_qforward(Q, K, V, qp, kv, kv, causal=True)
+    monkeypatch.delenv("MFA_DECODE")
+    assert maxerr(o, o2.cpu().numpy()) < 2e-3
+
+
 @pytest.mark.parametrize("B,H,Hkv,R,C,D,qp", [
     (2, 4, 4, 1, 1000, 128, P.FP16),
     (1, 8, 2, 3, 777, 64, P.BF16),     # GQA
