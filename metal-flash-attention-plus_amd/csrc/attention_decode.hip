@@ -33,26 +33,6 @@ __device__ __forceinline__ i16x8 widen_i8(uint32_t lo, uint32_t hi, float zp) {
   return __builtin_bit_cast(i16x8, dequant_fast<E, SRC_I8>(make_uint4(lo, hi, 0u, 0u), zp));
 }
 
-// 8 bytes holding nibble values n (0..15, from the INT4 V widening) -> 8 MFMA elements
-// n - zk4 (zk4 = zp + 8).  FP16: 0x64nn = 1024 + n by v_perm, no sign flip.
-template <class E>
-__device__ __forceinline__ i16x8 widen_u4(uint32_t lo, uint32_t hi, float zk4) {
-  if constexpr (E::prec == P_FP16) {
-    uint32_t w[4] = {__builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u),
-                     __builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u),
-                     __builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u),
-                     __builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u)};
-    const _Float16 m = (_Float16)(1024.0f + zk4);
-    const f16x2 mm = {m, m};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      w[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, w[k]) - mm);
-    return __builtin_bit_cast(i16x8, make_uint4(w[0], w[1], w[2], w[3]));
-  } else {
-    return widen_i8<E>(lo, hi, zk4);
-  }
-}
-
 // INT4 K fragments straight from the packed tile: 8 nibbles (n0 in the low nibble) -> 8 MFMA
 // elements n - 8 - zp (zk4 = zp + 8).  FP16: v_perm places the even nibbles n0 n2 n4 n6 and
 // the odd ones n1 n3 n5 n7 as the low bytes of 1024 + n (0x64nn) — one v_perm per pair, then a
@@ -132,16 +112,16 @@ constexpr int vm_wait(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
 // GEMMQuantization.swift:500-515), staged by LDS-DMA as stored.  K fragments are widened from
 // the packed tile in registers (nib_widen; each lane reads 16 consecutive elements = 8 bytes
 // for two k-steps, so the lane's k-step st covers d = 32·(st / 2) + 16·hh + 8·(st % 2) + j and
-// Q is loaded in that order; the packed K rows land XOR-swizzled by 16-byte chunk); the V tile
-// is widened in LDS to the INT8 tile layout (nibble n as the byte n, the zero point raised by
-// 8: the nibble encodes n - 8) and read by the INT8 loop's transposed reads.
+// Q is loaded in that order; the packed K rows land XOR-swizzled by 16-byte chunk); V^T
+// fragments come straight from the packed V tile (same swizzle) by ds_read_b64_tr_b4 and are
+// widened in registers the same way (the zero point raised by 8: the nibble encodes n - 8).
 template <class E, int DP, int SRC = SRC_I8>
 __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(DecodeParams dp) {
   const FwdParams& p = dp.f;
   constexpr bool I4 = SRC == SRC_I4;
-  // INT4 keeps two tiles in flight (three ring slots in the INT8 ring's bytes: the packed
-  // tiles are half as large).
-  constexpr int BK = 32, NSLOT = SRC == SRC_I4 ? 3 : 2, ND = DP / 32;
+  // INT4 keeps three tiles in flight (four ring slots in the INT8 ring's bytes: the packed
+  // tiles are half as large, and V is read from the packed tile too).
+  constexpr int BK = 32, NSLOT = SRC == SRC_I4 ? 4 : 2, ND = DP / 32;
   constexpr int ROWB = DP;                  // INT8 compute tile: one byte per element
   using T = Tile16<ROWB / 2>;               // [BK][ROWB bytes], 16-byte chunks XOR-swizzled
   constexpr int TILEB = BK * ROWB;          // one K or V compute tile
@@ -155,12 +135,10 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  // Per wave: NSLOT DMA slots (K at 2s·TILEBS, V after it); INT4 also the widened INT8 V tile
-  // after them (4·TILEB in all for both).
-  constexpr int WREG = NSLOT * 2 * TILEBS + (I4 ? TILEB : 0);
+  // Per wave: NSLOT DMA slots (K at 2s·TILEBS, V after it): 4·TILEB in all for both.
+  constexpr int WREG = NSLOT * 2 * TILEBS;
   static_assert(WREG == 4 * TILEB, "per-wave LDS region");
   char* const ring = smem + wave * WREG;
-  char* const conv = ring + NSLOT * 2 * TILEBS;  // INT4: the widened V tile
 
   const int split = blockIdx.x;
   const int u = blockIdx.y + gridDim.y * blockIdx.z;    // (b·H_kv + kvh)·nrt + rt
@@ -200,8 +178,6 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   // contiguous); lane l lands at byte 16·l of it = row n·RP + l / CPR, physical chunk l % CPR,
   // so it fetches logical chunk (l % CPR) ^ swz(row).  Rows past C and chunks past D read as
   // zeros (range-checked descriptor per piece, out-of-row chunks out of range).
-  // (INT4: the packed rows land unswizzled, as stored; the widening writes the swizzled INT8
-  // layout.)
   constexpr int CPR = ROWBS / 16;
   constexpr int SH = I4 ? 1 : 0;  // element -> byte offsets
   // Packed INT4 K rows: 16-byte chunk c of row r at physical chunk c ^ swz4(r), so the 8-byte
@@ -218,9 +194,8 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
     const int r = n * RP + lane / CPR;
     const int ch = I4 ? (lane % CPR) ^ swz4(r) : (lane % CPR) ^ T::swz(r);
     poff[n] = ch * 16 < (p.D >> SH) ? r * ssb + ch * 16 : 0x40000000;
-    // V: INT8 as K; INT4 unswizzled (the LDS widening reads its rows in order).
-    const int cv = I4 ? lane % CPR : ch;
-    voff[n] = cv * 16 < (p.D >> SH) ? r * ssb + cv * 16 : 0x40000000;
+    // V: the same chunk placement as K (INT4: the transposed 4-bit reads below).
+    voff[n] = ch * 16 < (p.D >> SH) ? r * ssb + ch * 16 : 0x40000000;
   }
   const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> SH);
   const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> SH);
@@ -241,37 +216,26 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
       lds_dma16(vhead + rv, max(vbytes - rv, 0), voff[n], kdst + TILEBS + n * 1024);
     }
   };
-  // INT4: the packed V tile of this slot widened into the INT8 compute tile (wave-private: the
-  // wave's own LDS accesses stay in order, no barrier).  A dword of 8 nibbles becomes the 8
-  // bytes n0..n7: the even and the odd nibbles masked out, then interleaved by two v_perm.
-  auto widen_i4_tile = [&](int slot) {
-    constexpr int NCP = ROWBS / 16, PER = BK * NCP / 64;
-    auto expand2 = [](uint32_t x, uint32_t& a, uint32_t& b) {
-      const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
-      a = __builtin_amdgcn_perm(hi, lo, 0x05010400u);  // n0 n1 n2 n3
-      b = __builtin_amdgcn_perm(hi, lo, 0x07030602u);  // n4 n5 n6 n7
-    };
-    const char* src = ring + slot * 2 * TILEBS + TILEBS;
-    char* dst = conv;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int idx = lane + 64 * j, r = idx / NCP, pc = idx % NCP;
-      const uint4 w = *reinterpret_cast<const uint4*>(src + r * ROWBS + pc * 16);
-      uint4 e0, e1;
-      expand2(w.x, e0.x, e0.y);
-      expand2(w.y, e0.z, e0.w);
-      expand2(w.z, e1.x, e1.y);
-      expand2(w.w, e1.z, e1.w);
-      *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc)) = e0;
-      *reinterpret_cast<uint4*>(dst + T::off(r, 2 * pc + 1)) = e1;
-    }
-  };
-
   // ds_read_b64_tr_b8 lanes (see attention_fwd_i8.hip): in each 16-lane group, lane 2j supplies
   // the row of key acc_row(j + 8s, hh) and receives column d0 + (lane & 15) of the 8 rows.
   const int trj = (lane & 15) >> 1;
   const int trg = (lane >> 4) & 1;
   const int trow0 = acc_row(trj, hh), trow1 = acc_row(trj + 8, hh);
+  // INT4 V^T fragments by ds_read_b64_tr_b4: in each 16-lane group lane r supplies row r (16
+  // nibbles = 16 d's of one key) and receives nibble (lane & 15) of all 16 rows, i.e. d =
+  // dt·32 + l32 for 16 keys: nibbles 0-7 are k-step 0's fragment, 8-15 k-step 1's.  The rows
+  // are chosen so that, after nib_widen's slot order (FP16: slot j <- nibble pi(j), pi = 0 2 4 6
+  // 1 3 5 7; BF16: natural), slot j of k-step ks holds key acc_row(8·ks + j, hh), the key order
+  // of the packed P.
+  int v4off = 0, v4sw = 0;
+  if constexpr (I4) {
+    const int r = lane & 15;
+    constexpr int PINV[8] = {0, 4, 1, 5, 2, 6, 3, 7};  // pi^-1
+    const int jj = E::prec == P_FP16 ? PINV[r & 7] : (r & 7);
+    const int key = acc_row(8 * (r >> 3) + jj, hh);
+    v4off = key * ROWBS + 8 * ((lane >> 4) & 1);
+    v4sw = swz4(key);
+  }
   const float zk = (float)(p.k.zp + (I4 ? 8 : 0)), zv = (float)(p.v.zp + (I4 ? 8 : 0));
 
   f32x16 o[ND];
@@ -279,24 +243,23 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   for (int dt = 0; dt < ND; ++dt) o[dt] = zero16();
   float m = -kFltMax, lh = 0.f;
 
-  if (mine > 0) issue(0, 0);
-  if (NSLOT == 3 && mine > 1) issue(1, 1);
+#pragma unroll
+  for (int n = 0; n < NSLOT - 1; ++n)
+    if (mine > n) issue(n, n);
   for (int i = 0; i < mine; ++i) {
     const int slot = i % NSLOT;
     if (i + NSLOT - 1 < mine) {
       issue(i + NSLOT - 1, (i + NSLOT - 1) % NSLOT);
       __builtin_amdgcn_s_waitcnt(vm_wait((NSLOT - 1) * 2 * NPC));  // tile i landed
-    } else if (NSLOT == 3 && i + 1 < mine) {
+    } else if (NSLOT >= 4 && i + 2 < mine) {
+      __builtin_amdgcn_s_waitcnt(vm_wait(4 * NPC));  // tiles i + 1, i + 2 still in flight
+    } else if (NSLOT >= 3 && i + 1 < mine) {
       __builtin_amdgcn_s_waitcnt(vm_wait(2 * NPC));  // tile i + 1 still in flight
     } else {
       wait_vm();
     }
-    const char* kt = ring + slot * 2 * TILEB;
-    const char* vt = kt + TILEB;
-    if constexpr (I4) {
-      widen_i4_tile(slot);
-      vt = conv;
-    }
+    const char* kt = ring + slot * 2 * TILEBS;
+    const char* vt = kt + TILEBS;
     const int t = k0 + BK * (wave + 4 * i);
 
     // S^T = K·Q^T: key l32 on the A operand's row, elements d = 16s + 8hh + j (INT4: the lane
@@ -354,17 +317,26 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[ks][j] = (short)E::from_f32(s[8 * ks + j]);
     // O^T += V^T·P^T.
+    if constexpr (I4) {
+      const char* vp = ring + slot * 2 * TILEBS + TILEBS;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt) {
-      const int col = dt * 32 + 16 * trg + 8 * (lane & 1);
+      for (int dt = 0; dt < ND; ++dt) {
+        const i32x2d w = __builtin_amdgcn_ds_read_tr4_b64_v2i32(
+            (__attribute__((address_space(3))) i32x2d*)(vp + v4off + 16 * (dt ^ v4sw)));
+        o[dt] = E::mma(nib_widen<E>((uint32_t)w[0], zv), pb[0], o[dt]);
+        o[dt] = E::mma(nib_widen<E>((uint32_t)w[1], zv), pb[1], o[dt]);
+      }
+    } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const char* pa = vt + T::off(ks ? trow1 : trow0, col >> 4) + (col & 15);
-        const i32x2d w = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-            (__attribute__((address_space(3))) i32x2d*)pa);
-        o[dt] = E::mma(I4 ? widen_u4<E>((uint32_t)w[0], (uint32_t)w[1], zv)
-                          : widen_i8<E>((uint32_t)w[0], (uint32_t)w[1], zv),
-                       pb[ks], o[dt]);
+      for (int dt = 0; dt < ND; ++dt) {
+        const int col = dt * 32 + 16 * trg + 8 * (lane & 1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const char* pa = vt + T::off(ks ? trow1 : trow0, col >> 4) + (col & 15);
+          const i32x2d w = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+              (__attribute__((address_space(3))) i32x2d*)pa);
+          o[dt] = E::mma(widen_i8<E>((uint32_t)w[0], (uint32_t)w[1], zv), pb[ks], o[dt]);
+        }
       }
     }
   }

@@ -587,8 +587,9 @@ def test_decode_causal(gpu, kv, B, H, Hkv, R, C, D, qp, monkeypatch):
 ])
 def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     # INT4 K/V cache at decode shapes on the split-KV kernel: the packed tiles are staged as
-    # stored and widened in LDS to the INT8 layout.  Held to the oracle on the dequantised
-    # values and to the generic dequant-on-load kernel (MFA_DECODE=0).
+    # stored and widened in registers (K by 8-byte row reads, V^T by 4-bit transposed LDS
+    # reads).  Held to the oracle on the dequantised values and to the generic dequant-on-load
+    # kernel (MFA_DECODE=0).
     rng = np.random.default_rng(R * 17 + C)
     Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
     K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
