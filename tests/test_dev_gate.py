@@ -19,7 +19,7 @@ KNOBS = {
     "MFA_DISABLE_FAST": "1", "MFA_FWD2_TUNE": "1", "MFA_SHARE_XCD": "0", "MFA_SHARE_DV": "0",
     "MFA_SHARE_NT": "0", "MFA_SHARE_SWI": "0", "MFA_SHARE_IMG": "0", "MFA_KV8": "0",
     "MFA_BWDQ_BYTES": "1", "MFA_NO_DEQUANT_PASS": "1", "MFA_KV_REGS": "0", "MFA_DECODE": "0",
-    "MFA_DECODE_MERGE": "1", "MFA_I8_BK": "1", "MFA_I8_SHARE": "0", "MFA_BWD256_BIGD": "1",
+    "MFA_DECODE_MERGE": "1", "MFA_DECODE16": "0", "MFA_I8_BK": "1", "MFA_I8_SHARE": "0", "MFA_BWD256_BIGD": "1",
     "MFA_GEMM_IMG": "0", "MFA_GEMM_NN": "1", "MFA_GEMM3": "0",
 }
 
@@ -52,6 +52,7 @@ for k in (K.forward, K.backwardQuery, K.backwardKeyValue):
     out["q256-%d" % int(k)] = names(mfa.quantized_plan(q256, k))
 dec = mfa.AttentionDescriptor.make(1, 8192, 128, low_precision=True, precision=P.FP16)
 out["decode"] = names(mfa.quantized_plan(mfa.quantized_descriptor(dec, P.FP16, P.INT8, P.INT8, B=32, H=16)))
+out["decode-i4"] = names(mfa.quantized_plan(mfa.quantized_descriptor(dec, P.FP16, P.INT4, P.INT4, B=32, H=16)))
 print(json.dumps(out))
 """
 

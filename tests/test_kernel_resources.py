@@ -20,7 +20,7 @@ _LLVM = "/opt/rocm/lib/llvm/bin"
 # attention_fwd_i8.hip, attention_fwd_kv8.hip, attention_decode.hip, attention_bwd_fast.hip,
 # attention_bigd.hip, attention_mla_latent.hip, kv_dequant.hip, gemm.hip, quantize.hip).
 HOT = ("mfa_fwd2_kernel", "mfa_fwd2_pair_kernel", "mfa_fwd2_share_kernel", "mfa_fwd2_stream_kernel",
-       "mfa_fwd_i8_kernel", "mfa_fwd2_kv8_kernel", "mfa_fwd_decode_kernel", "mfa_decode_merge",
+       "mfa_fwd_i8_kernel", "mfa_fwd2_kv8_kernel", "mfa_fwd_decode_kernel", "mfa_fwd_decode16_kernel", "mfa_decode_merge",
        "mfa_bwd_q_fast_kernel", "mfa_bwd_kv_fast_kernel", "mfa_fwd_bigd_kernel",
        "mfa_bwd_q_bigd_kernel", "mfa_mla", "mfa_kv_dequant_kernel", "mfa_gemm2_kernel",
        "mfa_gemm3_kernel", "qz_", "mfa_fwd_pipe_kernel", "mfa_fwd2_share_kv8_kernel")

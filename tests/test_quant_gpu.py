@@ -566,7 +566,7 @@ def test_decode_causal(gpu, kv, B, H, Hkv, R, C, D, qp, monkeypatch):
     base = mfa.AttentionDescriptor.make(R, C, D, causal=True, low_precision=True, precision=qp)
     desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
     names = [r["name"] for r in mfa.quantized_plan(desc)]
-    assert names[0].startswith("mfa_fwd_decode_kernel<"), names
+    assert names[0].startswith("mfa_fwd_decode"), names
     o, l, deq, _ = run_qforward(Q, K, V, qp, kv, kv, causal=True)
     ref = ol.attention(deq["Q"], deq["K"], deq["V"], causal=True)
     assert np.isfinite(o.cpu().numpy()).all()
@@ -584,19 +584,26 @@ def test_decode_causal(gpu, kv, B, H, Hkv, R, C, D, qp, monkeypatch):
     (2, 4, 1, 5, 300, 256, P.FP16),    # MQA, D 256
     (1, 16, 1, 4, 300, 128, P.FP16),   # two row tiles, one split: in-workgroup merge
     (1, 2, 2, 16, 4101, 128, P.BF16),  # 16 query rows, partial last tile
+    (1, 2, 2, 1, 33, 64, P.FP16),      # one partial 64-key tile
+    (1, 4, 4, 7, 70, 96, P.FP16),      # D 96 in the 128-wide tiles
 ])
 def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
-    # INT4 K/V cache at decode shapes on the split-KV kernel: the packed tiles are staged as
-    # stored and widened in registers (K by 8-byte row reads, V^T by 4-bit transposed LDS
-    # reads).  Held to the oracle on the dequantised values and to the generic dequant-on-load
-    # kernel (MFA_DECODE=0).
+    # INT4 K/V cache at decode shapes on the split-KV kernels: the packed tiles are staged as
+    # stored and widened in registers (K by row reads, V^T by 4-bit transposed LDS reads); at
+    # most 16 rows per kv head and D <= 128 take the 16x16x32 kernel.  Held to the oracle on
+    # the dequantised values, to the generic dequant-on-load kernel (MFA_DECODE=0) and, for
+    # the 16-row kernel, to the 32-row one (MFA_DECODE16=0).
     rng = np.random.default_rng(R * 17 + C)
     Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
     K, V = (rng.standard_normal((B, Hkv, C, D)).astype(np.float32) for _ in range(2))
     base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
     desc = mfa.quantized_descriptor(base, qp, P.INT4, P.INT4, B=B, H=H, Hkv=Hkv)
     names = [r["name"] for r in mfa.quantized_plan(desc)]
-    assert names[0].startswith("mfa_fwd_decode_kernel<") and names[0].endswith(", 2>"), names
+    d16 = (H // Hkv) * R <= 16 and D <= 128
+    if d16:
+        assert names[0].startswith("mfa_fwd_decode16_kernel<"), names
+    else:
+        assert names[0].startswith("mfa_fwd_decode_kernel<") and names[0].endswith(", 2>"), names
     o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT4, P.INT4)
     ref = ol.attention(deq["Q"], deq["K"], deq["V"])
     assert np.isfinite(o.cpu().numpy()).all()
@@ -606,6 +613,13 @@ def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     o2, _, _, _ = run_qforward(Q, K, V, qp, P.INT4, P.INT4)
     monkeypatch.delenv("MFA_DECODE")
     assert maxerr(o, o2.cpu().numpy()) < 2e-3
+    if d16:
+        monkeypatch.setenv("MFA_DECODE16", "0")
+        assert mfa.quantized_plan(desc)[0]["name"].startswith("mfa_fwd_decode_kernel<")
+        o3, l3, _, _ = run_qforward(Q, K, V, qp, P.INT4, P.INT4)
+        monkeypatch.delenv("MFA_DECODE16")
+        assert maxerr(o, o3.cpu().numpy()) < 2e-3
+        assert maxerr(l, l3.float().cpu().numpy()) < 7e-3
 
 
 def test_decode_int4_zero_points(gpu):
@@ -625,7 +639,7 @@ def test_decode_int4_zero_points(gpu):
     o = torch.empty((B, H, R, D), dtype=torch.float32, device=DEV)
     l = torch.empty((B, H, R), dtype=torch.float16, device=DEV)
     assert mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)[0]["name"].startswith(
-        "mfa_fwd_decode_kernel<")
+        "mfa_fwd_decode16_kernel<")
     mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
     torch.cuda.synchronize()
     Kd = (kn.astype(np.float32) - 8 - kz) * np.float32(ks)
