@@ -390,19 +390,21 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// INT4 K/V, at most 16 query rows per kv head (the usual decode step: S_q 1-16, GQA groups up
-// to 16 rows): the same split / partial / merge layout on v_mfma_f32_16x16x32, whose 16-query
-// output halves the per-key softmax work of the 32-row tile (a lane holds 16 scores per 64
-// keys instead of 16 per 32) and whose K operand rows are contiguous 16-byte reads:
-//   * 64-key tiles, each wave its own; K goes from HBM straight to registers (lane: key l16 of
-//     a 16-key block, bytes g·DP/8 .. g·DP/8 + DP/8 of its packed row: one wave load is 16
-//     whole rows), double-buffered one tile ahead; V by LDS-DMA into a 3-slot ring, two tiles
-//     ahead, its 16-byte chunks XOR-swizzled by (row >> 4);
-//   * S^T = K·Q^T: k-step dt of a lane covers d = g·DP/4 + 8·dt + kI4Perm[j] (nib_widen's
-//     order; Q loaded to match); the output holds key 16·kb + 4·g + e, query l16;
-//   * O^T += V^T·P^T with V^T fragments by ds_read_b64_tr_b4: lane r of each 16-lane group
-//     supplies the row of the key its slot needs (32·c + 16·(j >> 2) + 4·g + (j & 3) for
-//     nibble r = 8·c + pi(j)), so the P fragments are the S registers as they lie.
+// At most 16 query rows per kv head (the usual decode step: S_q 1-16, GQA groups up to 16
+// rows), D <= 128: the same split / partial / merge layout on v_mfma_f32_16x16x32, whose
+// 16-query output halves the per-key softmax work of the 32-row tile (a lane holds one score
+// per 4 keys instead of per 2) and whose K operand rows are contiguous reads:
+//   * key tiles of BK = 64 (INT4) / 32 (INT8), each wave its own; K goes from HBM straight to
+//     registers (lane: key l16 of a 16-key block, bytes g·ROWBS/4 .. (g+1)·ROWBS/4 of its
+//     row: one wave load is 16 whole rows), double-buffered one tile ahead; V by LDS-DMA into a
+//     3-slot ring, two tiles ahead, its 16-byte chunks XOR-swizzled per row (vsw);
+//   * S^T = K·Q^T: k-step dt of a lane covers d = g·DP/4 + 8·dt + j (INT4: + kI4Perm[j],
+//     nib_widen's order; Q loaded to match); the output holds key 16·kb + 4·g + e, query l16;
+//   * O^T += V^T·P^T with V^T fragments read transposed from the V tile (INT4
+//     ds_read_b64_tr_b4: lane r of each 16-lane group supplies the row of nibble slot r, key
+//     32·c + 16·(j >> 2) + 4·g + (j & 3) for r = 8·c + pi(j); INT8 ds_read_b64_tr_b8: lanes
+//     2j, 2j + 1 supply key 16·(j >> 2) + 4·g + (j & 3)), so the P fragments are the S
+//     registers as they lie.
 template <class E>
 __device__ __forceinline__ f32x4 mma16(i16x8 a, i16x8 b, f32x4 c) {
   if constexpr (E::prec == P_FP16)
@@ -427,22 +429,27 @@ __device__ __forceinline__ float xgroup_sum(float x) {
                         __builtin_bit_cast(float, (unsigned)r[1]));
 }
 
-template <int DP>
+template <int DP, int SRC>
 constexpr int decode16_lds() {
-  constexpr int ring = 4 * 3 * 64 * (DP / 2), merge = 4 * 16 * DP * 4 + 4 * 16 * 8;
+  constexpr int tile = (SRC == SRC_I4 ? 64 * (DP / 2) : 32 * DP);
+  constexpr int ring = 4 * 3 * tile, merge = 4 * 16 * DP * 4 + 4 * 16 * 8;
   return ring > merge ? ring : merge;
 }
 
-template <class E, int DP>
+template <class E, int DP, int SRC>
 __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams dp) {
   const FwdParams& p = dp.f;
-  constexpr int BK = 64, NV = 3, NDT = DP / 32, NDB = DP / 16;
-  constexpr int ROWBS = DP / 2;             // packed bytes per row
-  constexpr int TILEBS = BK * ROWBS;        // one packed 64-key tile
+  constexpr bool I4 = SRC == SRC_I4;
+  constexpr int BK = I4 ? 64 : 32, NKB = BK / 16, NV = 3, NDT = DP / 32, NDB = DP / 16;
+  constexpr int SH = I4 ? 1 : 0;            // element -> byte offsets
+  constexpr int ROWBS = DP >> SH;           // stored bytes per row
+  constexpr int TILEBS = BK * ROWBS;        // one stored key tile
   constexpr int NPV = TILEBS / 1024;        // V DMA pieces per tile
   constexpr int RP = 1024 / ROWBS;          // rows per piece
   constexpr int CPR = ROWBS / 16;           // 16-byte chunks per row
-  constexpr int KLB = DP / 8;               // K bytes per lane per 16-key block
+  constexpr int KLB = ROWBS / 4;            // K bytes per lane per 16-key block
+  constexpr int NKL = KLB >= 16 ? KLB / 16 : 1;  // K loads per block (b128, or one b64)
+  constexpr int NI = NPV + NKB * NKL;       // vm operations per tile
   static_assert(DP == 64 || DP == 128, "decode16 widths");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -452,11 +459,11 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   char* const ring = smem + wave * NV * TILEBS;
 
   const int split = blockIdx.x;
-  const int u = blockIdx.y + gridDim.y * blockIdx.z;    // (b·H_kv + kvh), one row tile
+  const int u = blockIdx.y + gridDim.y * blockIdx.z;    // b·H_kv + kvh (one row tile)
   const int kvh = u % p.Hkv, b = u / p.Hkv;
   const float c = p.c_log2;
 
-  // Q^T fragments: lane (query l16, group g), k-step dt: d = g·DP/4 + 8·dt + kI4Perm[j].
+  // Q^T fragments: lane (query l16, group g), k-step dt: d = g·DP/4 + 8·dt + (kI4Perm)[j].
   const int row = l16;
   const bool rvalid = row < dp.rows;
   const int qcol = rvalid ? row % p.R : 0x3fffffff;
@@ -471,58 +478,72 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
       const int d0 = g * (DP / 4) + 8 * dt;
       i16x8 v = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (rvalid && d0 < p.D) v = *reinterpret_cast<const i16x8*>(qrow + d0);
-      qf[dt] = i4_order<E>(v);
+      qf[dt] = I4 ? i4_order<E>(v) : v;
     }
   }
 
-  // Keys of this split: [k0, k1); this wave's tiles k0 + 64·(wave + 4i).
+  // Keys of this split: [k0, k1); this wave's tiles k0 + BK·(wave + 4i).
   const int k0 = split * dp.chunk;
   const int k1 = min(p.C, k0 + dp.chunk);
   const int nt = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
   const int mine = nt > wave ? (nt - wave + 3) / 4 : 0;
 
-  const int ssb = (int)(p.k.ss >> 1);
-  const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> 1);
-  const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> 1);
-  const int kbytes = (int)((int64_t)(p.C - 1) * ssb + (p.D >> 1));
-  const int vbytes = (int)((int64_t)(p.C - 1) * (p.v.ss >> 1) + (p.D >> 1));
-  // K row offsets of the lane's four 16-key blocks (bytes past D: out of range, read as 0).
-  const int kcol = g * KLB < (p.D >> 1) ? g * KLB : 0x40000000;
-  int koff[4];
+  const int ssb = (int)(p.k.ss >> SH);
+  const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> SH);
+  const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> SH);
+  const int kbytes = (int)((int64_t)(p.C - 1) * ssb + (p.D >> SH));
+  const int vbytes = (int)((int64_t)(p.C - 1) * (p.v.ss >> SH) + (p.D >> SH));
+  // K row offsets of the lane's 16-key blocks (bytes past D: out of range, read as 0).
+  const int kcol = g * KLB < (p.D >> SH) ? g * KLB : 0x40000000;
+  int koff[NKB];
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) koff[kb] = (16 * kb + l16) * ssb + kcol;
+  for (int kb = 0; kb < NKB; ++kb) koff[kb] = (16 * kb + l16) * ssb + kcol;
+  // V chunk swizzle: the 16 (INT4) / 8 + 8 (INT8) rows one transposed read gathers into a
+  // 32-lane half spread over the banks (INT4: 2-way at most; INT8: conflict-free).
+  auto vsw = [](int r) {
+    if constexpr (I4) return (r >> 4) & (CPR - 1);
+    else if constexpr (CPR == 8) return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | (((r >> 4) & 1) << 2);
+    else return ((r >> 2) & 1) | (((r >> 4) & 1) << 1);
+  };
   // V DMA: piece n holds rows n·RP .. n·RP + RP - 1; lane l lands at physical chunk l % CPR of
   // row n·RP + l / CPR and fetches logical chunk (l % CPR) ^ vsw(row).
-  auto vsw = [](int r) { return (r >> 4) & (CPR - 1); };
   int voff[NPV];
 #pragma unroll
   for (int n = 0; n < NPV; ++n) {
     const int r = n * RP + lane / CPR;
     const int ch = (lane % CPR) ^ vsw(r);
-    voff[n] = ch * 16 < (p.D >> 1) ? r * ssb + ch * 16 : 0x40000000;
+    voff[n] = ch * 16 < (p.D >> SH) ? r * ssb + ch * 16 : 0x40000000;
   }
-  // Transposed V reads: lane r of the group supplies the row of nibble slot r.
-  int v4row, v4sw;
+  // Transposed V reads: the row this lane supplies, and its swizzle.
+  int vtrow, vtsw;
   {
     constexpr int PINV[8] = {0, 4, 1, 5, 2, 6, 3, 7};  // kI4Perm^-1
-    const int r = l16;
-    const int j = E::prec == P_FP16 ? PINV[r & 7] : (r & 7);
-    const int key = 32 * (r >> 3) + 16 * (j >> 2) + 4 * g + (j & 3);
-    v4row = key * ROWBS;
-    v4sw = vsw(key);
+    int key;
+    if constexpr (I4) {
+      const int j = E::prec == P_FP16 ? PINV[l16 & 7] : (l16 & 7);
+      key = 32 * (l16 >> 3) + 16 * (j >> 2) + 4 * g + (j & 3);
+    } else {
+      const int j = l16 >> 1;
+      key = 16 * (j >> 2) + 4 * g + (j & 3);
+    }
+    vtrow = key * ROWBS + (I4 ? 0 : 8 * (l16 & 1));
+    vtsw = vsw(key);
   }
-  const float zk = (float)(p.k.zp + 8), zv = (float)(p.v.zp + 8);
+  const float zk = (float)(p.k.zp + (I4 ? 8 : 0)), zv = (float)(p.v.zp + (I4 ? 8 : 0));
 
-  uint32_t ka[4][NDT], kn[4][NDT];
+  uint32_t ka[NKB][KLB / 4], kn[NKB][KLB / 4];
 #define DEC16_KLOAD(KR, TI)                                                                       \
   {                                                                                              \
     const int tb_ = (k0 + BK * (wave + 4 * (TI))) * ssb;                                         \
     const __amdgpu_buffer_rsrc_t rs_ = __builtin_amdgcn_make_buffer_rsrc(                        \
         (void*)(khead + tb_), (short)0, max(kbytes - tb_, 0), 0x00020000);                       \
-    _Pragma("unroll") for (int kb = 0; kb < 4; ++kb) {                                           \
-      if constexpr (NDT == 4) {                                                                  \
-        const auto a_ = __builtin_amdgcn_raw_buffer_load_b128(rs_, koff[kb], 0, 0);              \
-        KR[kb][0] = a_[0]; KR[kb][1] = a_[1]; KR[kb][2] = a_[2]; KR[kb][3] = a_[3];              \
+    _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb) {                                         \
+      if constexpr (KLB >= 16) {                                                                 \
+        _Pragma("unroll") for (int x = 0; x < NKL; ++x) {                                        \
+          const auto a_ = __builtin_amdgcn_raw_buffer_load_b128(rs_, koff[kb] + 16 * x, 0, 0);   \
+          KR[kb][4 * x] = a_[0]; KR[kb][4 * x + 1] = a_[1];                                      \
+          KR[kb][4 * x + 2] = a_[2]; KR[kb][4 * x + 3] = a_[3];                                  \
+        }                                                                                        \
       } else {                                                                                   \
         const auto a_ = __builtin_amdgcn_raw_buffer_load_b64(rs_, koff[kb], 0, 0);               \
         KR[kb][0] = a_[0]; KR[kb][1] = a_[1];                                                    \
@@ -542,35 +563,39 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   float m = -kFltMax, lh = 0.f;
 
   // Issue order V(0) K(0) V(1), then per tile i: K(i + 1) V(i + 2): V(i) always precedes K(i),
-  // so waiting for K(i) (a counted vmcnt) covers both.
+  // so one counted vmcnt wait for K(i) covers both.
 #define DEC16_STEP(KC, KN, I)                                                                     \
   {                                                                                              \
     const int ii = (I);                                                                          \
     if (ii + 1 < mine) DEC16_KLOAD(KN, ii + 1);                                                  \
     if (ii + 2 < mine) {                                                                         \
       vissue(ii + 2);                                                                            \
-      __builtin_amdgcn_s_waitcnt(vm_wait(2 * NPV + 4));                                          \
+      __builtin_amdgcn_s_waitcnt(vm_wait(NI + NPV));                                             \
     } else if (ii + 1 < mine) {                                                                  \
-      __builtin_amdgcn_s_waitcnt(vm_wait(NPV + 4));                                              \
+      __builtin_amdgcn_s_waitcnt(vm_wait(NI));                                                   \
     } else {                                                                                     \
       __builtin_amdgcn_s_waitcnt(vm_wait(0));                                                    \
     }                                                                                            \
     const char* vs = ring + (ii % NV) * TILEBS;                                                  \
     const int t = k0 + BK * (wave + 4 * ii);                                                     \
-    f32x4 sc[4];                                                                                 \
-    _Pragma("unroll") for (int kb = 0; kb < 4; ++kb) {                                           \
+    f32x4 sc[NKB];                                                                               \
+    _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb) {                                         \
       sc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};                                                        \
-      _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt)                                         \
-        sc[kb] = mma16<E>(nib_widen<E>(KC[kb][dt], zk), qf[dt], sc[kb]);                         \
+      _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt) {                                       \
+        if constexpr (I4)                                                                        \
+          sc[kb] = mma16<E>(nib_widen<E>(KC[kb][dt], zk), qf[dt], sc[kb]);                       \
+        else                                                                                     \
+          sc[kb] = mma16<E>(widen_i8<E>(KC[kb][2 * dt], KC[kb][2 * dt + 1], zk), qf[dt], sc[kb]); \
+      }                                                                                          \
     }                                                                                            \
     if (t + BK > k1 || (p.mask.causal && t + BK - 1 > qcol)) {                                   \
       const int last = (p.mask.causal ? min(k1 - 1, qcol) : k1 - 1) - t;                         \
-      _Pragma("unroll") for (int kb = 0; kb < 4; ++kb)                                           \
+      _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                         \
         _Pragma("unroll") for (int e = 0; e < 4; ++e)                                            \
           sc[kb][e] = 16 * kb + 4 * g + e > last ? -__builtin_inff() : sc[kb][e];                \
     }                                                                                            \
     float mx = fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3]));                      \
-    _Pragma("unroll") for (int kb = 1; kb < 4; ++kb)                                             \
+    _Pragma("unroll") for (int kb = 1; kb < NKB; ++kb)                                           \
       _Pragma("unroll") for (int e = 0; e < 4; ++e) mx = fmaxf(mx, sc[kb][e]);                   \
     mx = xgroup_max(mx) * c;                                                                     \
     if (__any(mx > m)) {                                                                         \
@@ -581,25 +606,31 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
       _Pragma("unroll") for (int db = 0; db < NDB; ++db) o[db] *= corr;                          \
     }                                                                                            \
     float rs = 0.f;                                                                              \
-    _Pragma("unroll") for (int kb = 0; kb < 4; ++kb)                                             \
+    _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                           \
       _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                            \
         const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e], c, -m));               \
         sc[kb][e] = pv;                                                                          \
         rs += pv;                                                                                \
       }                                                                                          \
     lh += rs;                                                                                    \
-    i16x8 pb[2];                                                                                 \
-    _Pragma("unroll") for (int cc = 0; cc < 2; ++cc)                                             \
+    i16x8 pb[NKB / 2];                                                                           \
+    _Pragma("unroll") for (int cc = 0; cc < NKB / 2; ++cc)                                       \
       _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                            \
         pb[cc][e] = (short)E::from_f32(sc[2 * cc][e]);                                           \
         pb[cc][4 + e] = (short)E::from_f32(sc[2 * cc + 1][e]);                                   \
       }                                                                                          \
     _Pragma("unroll") for (int db = 0; db < NDB; ++db) {                                         \
-      const i32x2d w = __builtin_amdgcn_ds_read_tr4_b64_v2i32(                                   \
-          (__attribute__((address_space(3))) i32x2d*)(vs + v4row + 16 * ((db >> 1) ^ v4sw) +     \
-                                                      8 * (db & 1)));                            \
-      o[db] = mma16<E>(nib_widen<E>((uint32_t)w[0], zv), pb[0], o[db]);                          \
-      o[db] = mma16<E>(nib_widen<E>((uint32_t)w[1], zv), pb[1], o[db]);                          \
+      if constexpr (I4) {                                                                        \
+        const i32x2d w = __builtin_amdgcn_ds_read_tr4_b64_v2i32(                                 \
+            (__attribute__((address_space(3))) i32x2d*)(vs + vtrow + 16 * ((db >> 1) ^ vtsw) +   \
+                                                        8 * (db & 1)));                          \
+        o[db] = mma16<E>(nib_widen<E>((uint32_t)w[0], zv), pb[0], o[db]);                        \
+        o[db] = mma16<E>(nib_widen<E>((uint32_t)w[1], zv), pb[NKB / 2 - 1], o[db]);              \
+      } else {                                                                                   \
+        const i32x2d w = __builtin_amdgcn_ds_read_tr8_b64_v2i32(                                 \
+            (__attribute__((address_space(3))) i32x2d*)(vs + vtrow + 16 * (db ^ vtsw)));         \
+        o[db] = mma16<E>(widen_i8<E>((uint32_t)w[0], (uint32_t)w[1], zv), pb[0], o[db]);         \
+      }                                                                                          \
     }                                                                                            \
   }
 
@@ -685,7 +716,9 @@ void decode_layout(int B, int Hkv, int rows, int C, int* nrt, int* nsplit, int* 
   *nrt = (rows + 31) / 32;
   const int units = B * Hkv * *nrt;
   const int tiles = (C + 31) / 32;
-  int ns = (512 + units - 1) / units;
+  const char* wg = dev_env("MFA_DECODE_WGS");  // A/B: workgroups to aim for
+  const int target = wg ? atoi(wg) : 512;
+  int ns = (target + units - 1) / units;
   if (ns > tiles / 16) ns = tiles / 16;
   if (ns < 1) ns = 1;
   const int per = (tiles + ns - 1) / ns;  // tiles per split, rounded to whole 4-wave rounds
@@ -729,12 +762,16 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
   dp.fused = decode_fused(dp.nsplit);
   if (!dp.fused && !workspace) return hipErrorInvalidValue;
   hipError_t e = hipErrorNotSupported;
-  // INT4 with at most 16 rows per kv head: the 16x16x32 kernel (MFA_DECODE16=0: the 32-row one).
+  // At most 16 rows per kv head, D <= 128: the 16x16x32 kernel (MFA_DECODE16=0: the 32-row
+  // one; =4: INT4 only).
   const char* d16 = dev_env("MFA_DECODE16");
-  if (i4 && dp.rows <= 16 && DP <= 128 && !(d16 && d16[0] == '0')) {
+  if (dp.rows <= 16 && DP <= 128 && !(d16 && d16[0] == '0') && (i4 || !(d16 && d16[0] == '4'))) {
 #define MFA_DEC16(ELEM, EE, DPV)                                                               \
     if (elem == ELEM && DP == DPV)                                                             \
-      e = launch(mfa_fwd_decode16_kernel<EE, DPV>, grid, dim3(256), decode16_lds<DPV>(), stream, dp);
+      e = i4 ? launch(mfa_fwd_decode16_kernel<EE, DPV, SRC_I4>, grid, dim3(256),               \
+                      decode16_lds<DPV, SRC_I4>(), stream, dp)                                 \
+             : launch(mfa_fwd_decode16_kernel<EE, DPV, SRC_I8>, grid, dim3(256),               \
+                      decode16_lds<DPV, SRC_I8>(), stream, dp);
     MFA_DEC16(P_FP16, F16, 64)
     MFA_DEC16(P_FP16, F16, 128)
     MFA_DEC16(P_BF16, BF16, 64)

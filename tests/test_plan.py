@@ -143,7 +143,7 @@ def test_quantized_plans():
     dec = mfa.AttentionDescriptor.make(16, 8192, 128, low_precision=True, precision=P.FP16)
     qd = mfa.quantized_descriptor(dec, P.FP16, P.INT8, P.INT8, B=1, H=4)
     names = [r["name"] for r in mfa.quantized_plan(qd)]
-    assert names == ["mfa_fwd_decode_kernel<F16, 128, 1>", "mfa_decode_merge_kernel"], names
+    assert names == ["mfa_fwd_decode16_kernel<F16, 128, 1>", "mfa_decode_merge_kernel"], names
 
 
 def test_kv8_override_takes_the_dequant_pass(monkeypatch):
@@ -331,4 +331,4 @@ def test_decode_bench_shape_is_one_launch():
     for R in (1, 16):
         base = mfa.AttentionDescriptor.make(R, 8192, 128, low_precision=True, precision=P.FP16)
         desc = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=32, H=16)
-        assert [r["name"] for r in mfa.quantized_plan(desc)] == ["mfa_fwd_decode_kernel<F16, 128, 1>"]
+        assert [r["name"] for r in mfa.quantized_plan(desc)] == ["mfa_fwd_decode16_kernel<F16, 128, 1>"]

@@ -520,6 +520,8 @@ def test_integer_matmul_c3_heads(gpu):
     (1, 16, 1, 4, 2048, 128, P.BF16),  # 64 rows per kv head: two row tiles
     (1, 16, 1, 4, 300, 128, P.FP16),   # two row tiles, one split: in-workgroup merge
     (1, 2, 2, 1, 33, 64, P.FP16),      # one partial tile
+    (1, 4, 4, 7, 70, 96, P.BF16),      # D 96 in the 128-wide tiles
+    (2, 4, 2, 8, 2500, 128, P.FP16),   # GQA, 16 rows, split path
 ])
 def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     rng = np.random.default_rng(R * 13 + C)
@@ -528,7 +530,8 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
     desc = mfa.quantized_descriptor(base, qp, P.INT8, P.INT8, B=B, H=H, Hkv=Hkv)
     names = [r["name"] for r in mfa.quantized_plan(desc)]
-    assert names[0].startswith("mfa_fwd_decode_kernel<"), names
+    d16 = (H // Hkv) * R <= 16 and D <= 128
+    assert names[0].startswith("mfa_fwd_decode16_kernel<" if d16 else "mfa_fwd_decode_kernel<"), names
     # One key split per unit: the workgroup merges its waves in LDS (one launch); more
     # splits take the merge pass.
     assert names[1:] in ([], ["mfa_decode_merge_kernel"]), names
@@ -541,6 +544,13 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     o2, _, _, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
     monkeypatch.delenv("MFA_DECODE")
     assert maxerr(o, o2.cpu().numpy()) < 2e-3
+    if d16:  # the 16-row kernel against the 32-row one
+        monkeypatch.setenv("MFA_DECODE16", "0")
+        assert mfa.quantized_plan(desc)[0]["name"].startswith("mfa_fwd_decode_kernel<")
+        o4, l4, _, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
+        monkeypatch.delenv("MFA_DECODE16")
+        assert maxerr(o, o4.cpu().numpy()) < 2e-3
+        assert maxerr(l, l4.float().cpu().numpy()) < 7e-3
     if len(names) == 1:  # the in-workgroup merge equals the merge pass bit for bit
         monkeypatch.setenv("MFA_DECODE_MERGE", "1")
         assert [r["name"] for r in mfa.quantized_plan(desc)][1:] == ["mfa_decode_merge_kernel"]
@@ -665,7 +675,7 @@ def test_decode_nonzero_zero_point(gpu):
     o = torch.empty((B, H, R, D), dtype=torch.float32, device=DEV)
     l = torch.empty((B, H, R), dtype=torch.float16, device=DEV)
     assert mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)[0]["name"].startswith(
-        "mfa_fwd_decode_kernel<")
+        "mfa_fwd_decode16_kernel<")
     mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
     torch.cuda.synchronize()
     Kd = (kq.astype(np.float32) - kz) * np.float32(ks)
