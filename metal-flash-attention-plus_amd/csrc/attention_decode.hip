@@ -716,9 +716,7 @@ void decode_layout(int B, int Hkv, int rows, int C, int* nrt, int* nsplit, int* 
   *nrt = (rows + 31) / 32;
   const int units = B * Hkv * *nrt;
   const int tiles = (C + 31) / 32;
-  const char* wg = dev_env("MFA_DECODE_WGS");  // A/B: workgroups to aim for
-  const int target = wg ? atoi(wg) : 512;
-  int ns = (target + units - 1) / units;
+  int ns = (512 + units - 1) / units;
   if (ns > tiles / 16) ns = tiles / 16;
   if (ns < 1) ns = 1;
   const int per = (tiles + ns - 1) / ns;  // tiles per split, rounded to whole 4-wave rounds
