@@ -59,7 +59,8 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   char* const sv = smem + 2 * TILEB;      // 16-bit V slots 0, 1
 
   const int BH = p.B * p.H;
-  const int pi = blockIdx.x / BH;
+  // Causal: the heaviest pairs first (balance over the grid).
+  const int pi = p.mask.causal ? (p.nblk + 1) / 2 - 1 - (int)(blockIdx.x / BH) : blockIdx.x / BH;
   const int bh = blockIdx.x % BH;
   const int b = bh / p.H, h = bh % p.H, kvh = h % p.Hkv;
   const float c = p.c_log2;
@@ -68,7 +69,11 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   constexpr int ESH = SRC == SRC_I8 ? 0 : 1;
   const char* khead = (const char*)p.k.ptr + (((int64_t)b * p.k.sb + (int64_t)kvh * p.k.sh) >> ESH);
   const char* vhead = (const char*)p.v.ptr + (((int64_t)b * p.v.sb + (int64_t)kvh * p.v.sh) >> ESH);
-  const int n = (p.C + BK - 1) / BK;
+  // Key tiles [kbeg, kend) of the pair's 256 rows (causal / window: the tiles some row of the
+  // pair sees; the host routes these masks here only when skipping is exact, skip_ok).
+  int kbeg, kend;
+  key_range(p, 2 * pi * BQ, 2 * BQ, BK, &kbeg, &kend);
+  const int n = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const G geo(tid);
   const int cr = geo.r, ch0 = geo.ch0;
   const bool cvalid = geo.col < p.D;
@@ -142,10 +147,10 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   // its widening into tile s + 1's slot has been issued, one step ahead of its use.
   uint4 rk, rv;
   if constexpr (RAWLDS) {
-    dmak(0, 0);
-    dmav(0, 0);
-    dmak(BK, 1);
-    dmav(BK, 1);
+    dmak(kbeg, 0);
+    dmav(kbeg, 0);
+    dmak(kbeg + BK, 1);
+    dmav(kbeg + BK, 1);
     load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
     wait_vm();
     __asm__ __volatile__("" ::: "memory");
@@ -155,8 +160,8 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
       widen_half(sv, raw_read(rawb + 2 * RSLOT, hf), zv, hf);
     }
   } else {
-    rk = loadk(0);
-    rv = loadv(0);
+    rk = loadk(kbeg);
+    rv = loadv(kbeg);
     load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
   }
   prescale_q2<E, DP>(qf, c);
@@ -167,21 +172,21 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
       widen(sk, rk, zk, H1());
       widen(sv, rv, zv, H1());
     }
-    rk = loadk(BK);
-    rv = loadv(BK);
+    rk = loadk(kbeg + BK);
+    rv = loadv(kbeg + BK);
   }
   __syncthreads();
 
   RowState<DP> st;
   st.init();
-  const int wsz = 0x3fffffff;
+  const int wsz = p.mask.window_size > 0x3fffffffu ? 0x3fffffff : (int)p.mask.window_size;
   // Step s widens tile s + 1 into its 16-bit slots between the MFMAs of tile s.  On the last
   // steps the widening writes stale bytes into the slot of a tile already consumed: harmless,
   // and the MFMA chains stay branch-free.
   for (int s = 0; s < n; ++s) {
     const int cur = s & 1, nx = cur ^ 1;
-    const int t = s * BK;
-    const bool mask_tile = t + BK > p.C;
+    const int t = kbeg + s * BK;
+    const bool mask_tile = (t + BK > p.C) || (p.mask.causal && t + BK - 1 > q0) || p.mask.window;
     f32x16 sc[BK / 32];
     i16x8 pb[BK / 16];
     char* const knext = sk + nx * TILEB;

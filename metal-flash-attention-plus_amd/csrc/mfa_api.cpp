@@ -748,8 +748,10 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
   if (p.k.bscale || p.v.bscale) return false;
   if ((DP != 64 && DP != 128 && DP != 256) || p.D % 16 != 0 || !(p.c_log2 > 0.f)) return false;
   const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
-  if (p.mask.window || p.mask.amask || p.mask.ranges) return false;
-  if (p.mask.causal && DP != 128) return false;  // causal: the mirrored schedule at D = 128
+  if (p.mask.amask || p.mask.ranges) return false;
+  // Causal / window: tiles no row of a block sees are skipped, exact only when no row is
+  // masked everywhere (skip_ok).
+  if ((p.mask.causal || p.mask.window) && !p.mask.skip_ok) return false;
   if (p.q.sd != 1 || !p.q.vec || p.o_sd != 1) return false;
   if (p.k.sd != 1 || p.v.sd != 1) return false;
   for (const mfa::Operand* o : {&p.k, &p.v})
@@ -884,9 +886,13 @@ extern "C" mfa_status_t mfa_quantized_forward(const mfa_quantized_descriptor_t* 
     if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (decode) launch");
   }
   if (kv8_eligible(p, elem, qp, kp, vp, DP)) {
-    const hipError_t e =
-        p.mask.causal ? mfa::fwd_share_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream)
-                      : mfa::fwd_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream);
+    // Causal at D = 128: the mirrored shared-tile schedule where it applies; otherwise (and
+    // for window masks, D = 64 / 256) the adjacent-pair on-load kernel with the masks.
+    hipError_t e = hipErrorNotSupported;
+    if (p.mask.causal && !p.mask.window)
+      e = mfa::fwd_share_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream);
+    if (e == hipErrorNotSupported)
+      e = mfa::fwd_kv8_dispatch(p, elem, DP, src_kind(kp), (hipStream_t)stream);
     if (e != hipErrorNotSupported) return hip_status(e, "mfa_fwd (INT8 K/V on load) launch");
   }
   int kvsrc = src_kind(kp);

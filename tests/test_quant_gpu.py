@@ -817,6 +817,63 @@ def test_kv8_causal_on_load(gpu, kv, B, H, Hkv, R, C, zps, qp, monkeypatch):
     assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
 
 
+# Causal (D = 64 / 256, and D = 128 where the mirrored schedule does not apply) and sliding
+# window masks on the adjacent-pair on-load kernel (attention_fwd_kv8.hip): the pair stages
+# only the key tiles some row of it sees (skip_ok), masked per row like the 16-bit kernels.
+# Held to the oracle on the dequantised values and to the pass + 16-bit path (MFA_KV8=0).
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,causal,window,qp", [
+    (1, 4, 4, 640, 640, 64, True, None, P.FP16),
+    (1, 2, 1, 520, 700, 256, True, None, P.BF16),     # ragged rows, MQA, more keys than rows
+    (2, 2, 2, 1024, 1024, 256, False, 300, P.FP16),  # window (the sparsity patterns are exclusive)
+    (1, 4, 2, 900, 900, 128, False, 200, P.BF16),    # window only (rows keep keys >= r - 200)
+    (4, 48, 48, 1024, 1024, 128, True, None, P.FP16),  # 1,536 blocks: not the mirrored schedule
+])
+def test_kv8_masked_on_load(gpu, kv, B, H, Hkv, R, C, D, causal, window, qp, monkeypatch):
+    rng = np.random.default_rng(R + 3 * C + D)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    lim = 120 if kv == P.INT8 else 8
+    kq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    vq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    ks, vs, zps = 0.015, 0.02, (3, -2)
+    base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, window=window, low_precision=True,
+                                        precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, qp), qp)
+    if kv == P.INT8:
+        kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
+    else:
+        pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
+        kt, vt = tdev(pack(kq.astype(np.int32)), torch.uint8), tdev(pack(vq.astype(np.int32)), torch.uint8)
+    tk = mfa.quantized_tensor(kt, kv, scale=ks, zero_point=zps[0])
+    tv = mfa.quantized_tensor(vt, kv, scale=vs, zero_point=zps[1])
+    names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    assert names[0].startswith("mfa_fwd2_kv8_kernel<"), names
+
+    def run():
+        o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
+        l = torch.full((B, H, R), float("nan"), dtype=torch.float16, device=DEV)
+        mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+        torch.cuda.synchronize()
+        return o.cpu().numpy(), l.float().cpu().numpy()
+
+    o1, l1 = run()
+    monkeypatch.setenv("MFA_KV8", "0")
+    o2, l2 = run()
+    monkeypatch.delenv("MFA_KV8")
+    kd = ((kq.astype(np.float32) - zps[0]) * np.float32(ks)).astype(np.float32)
+    vd = ((vq.astype(np.float32) - zps[1]) * np.float32(vs)).astype(np.float32)
+    Qs = seen(Q, qp)
+    assert np.isfinite(o1).all()
+    for h in sorted({0, H - 1}):
+        ref = ol.attention(Qs[:, h:h + 1], kd[:, h % Hkv:h % Hkv + 1], vd[:, h % Hkv:h % Hkv + 1],
+                           causal=causal, window=window)
+        assert maxerr(o1[:, h:h + 1], ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max()), h
+        assert maxerr(l1[:, h:h + 1], ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max(), h
+    assert maxerr(o1, o2) < 2e-3 * max(1.0, np.abs(o2).max())
+    assert maxerr(l1, l2) < 7e-3 + 2 ** -10 * np.abs(l2).max()  # L is stored in fp16
+
+
 def _ref_dequant_transposed_block(e, B, H, S, D, bs, scales):
     """The reference's block lookup for a transposed quantised operand, written out per element
     (AttentionKernel+Accumulate.swift:461-472, AttentionKernel+OuterProduct.swift:301-316):

@@ -8,6 +8,7 @@ import os
 os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import sys
 
+import numpy as np
 import torch
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,11 +26,16 @@ def main():
              ("D64 fp16", 1, 32, 8192, 64, P.FP16, False), ("C5 fp16", 2, 32, 4096, 256, P.FP16, False),
              ("C5 bf16", 2, 32, 4096, 256, P.BF16, False),
              ("C2c fp16", 1, 16, 4096, 128, P.FP16, True), ("C2c bf16", 1, 16, 4096, 128, P.BF16, True),
-             ("S8kc fp16", 1, 16, 8192, 128, P.FP16, True)]
+             ("S8kc fp16", 1, 16, 8192, 128, P.FP16, True),
+             ("D64c fp16", 1, 32, 8192, 64, P.FP16, True), ("C5c fp16", 2, 32, 4096, 256, P.FP16, True),
+             ("C5c bf16", 2, 32, 4096, 256, P.BF16, True), ("B4c fp16", 4, 32, 4096, 128, P.FP16, True),
+             ("S8kw fp16", 1, 16, 8192, 128, P.FP16, False, 1024),
+             ("C5w bf16", 2, 32, 4096, 256, P.BF16, False, 512)]
     if len(sys.argv) > 1:
         cases = [c for c in cases if any(c[0].startswith(x) for x in sys.argv[1].split(","))]
     for kv in (P.INT8, P.INT4):
-        for name, B, H, S, D, qp, causal in cases:
+        for name, B, H, S, D, qp, causal, *win in cases:
+            win = win[0] if win else None
             tdt = torch.float16 if qp == P.FP16 else torch.bfloat16
             q = ((torch.rand((B, H, S, D), generator=g, device=dev) * 2 - 1)).to(tdt)
             nb = D if kv == P.INT8 else D // 2
@@ -37,14 +43,17 @@ def main():
             v = torch.randint(0, 256, (B, H, S, nb), generator=g, device=dev, dtype=torch.uint8)
             o = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
             l = torch.empty((B, H, S), dtype=torch.float16, device=dev)
-            base = mfa.AttentionDescriptor.make(S, S, D, causal=causal, low_precision=True,
+            base = mfa.AttentionDescriptor.make(S, S, D, causal=causal, window=win, low_precision=True,
                                                 precision=qp)
             desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H)
             tq = mfa.quantized_tensor(q, qp)
             tk = mfa.quantized_tensor(k, kv, scale=0.01)
             tv = mfa.quantized_tensor(v, kv, scale=0.01)
             qa = mfa.QuantizedAttention()
-            fl = 4.0 * B * H * S * S * D * (0.5 * (S + 1) / S if causal else 1.0)
+            r = np.arange(S)
+            lo = np.maximum(0, r - win) if win is not None else np.zeros(S, dtype=np.int64)
+            hi = np.minimum(S - 1, r) if causal else np.full(S, S - 1)
+            fl = 4.0 * B * H * D * float(np.maximum(hi - lo + 1, 0).sum())
 
             def run(onload):
                 if onload:
