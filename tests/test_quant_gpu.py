@@ -543,7 +543,8 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     monkeypatch.setenv("MFA_DECODE", "0")
     o2, _, _, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
     monkeypatch.delenv("MFA_DECODE")
-    assert maxerr(o, o2.cpu().numpy()) < 2e-3
+    # Both paths sit within the oracle tolerance, so within twice it of each other.
+    assert maxerr(o, o2.cpu().numpy()) < 4e-3 * max(1.0, np.abs(ref["O"]).max())
     if d16:  # the 16-row kernel against the 32-row one
         monkeypatch.setenv("MFA_DECODE16", "0")
         assert mfa.quantized_plan(desc)[0]["name"].startswith("mfa_fwd_decode_kernel<")
@@ -585,7 +586,9 @@ def test_decode_causal(gpu, kv, B, H, Hkv, R, C, D, qp, monkeypatch):
     monkeypatch.setenv("MFA_DECODE", "0")
     o2, _, _, _ = run_qforward(Q, K, V, qp, kv, kv, causal=True)
     monkeypatch.delenv("MFA_DECODE")
-    assert maxerr(o, o2.cpu().numpy()) < 2e-3
+    assert maxerr(o2, ref["O"]) < 2e-3 * max(1.0, np.abs(ref["O"]).max())
+    # Both paths sit within the oracle tolerance, so within twice it of each other.
+    assert maxerr(o, o2.cpu().numpy()) < 4e-3 * max(1.0, np.abs(ref["O"]).max())
 
 
 @pytest.mark.parametrize("B,H,Hkv,R,C,D,qp", [
@@ -622,7 +625,8 @@ def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     monkeypatch.setenv("MFA_DECODE", "0")
     o2, _, _, _ = run_qforward(Q, K, V, qp, P.INT4, P.INT4)
     monkeypatch.delenv("MFA_DECODE")
-    assert maxerr(o, o2.cpu().numpy()) < 2e-3
+    # Both paths sit within the oracle tolerance, so within twice it of each other.
+    assert maxerr(o, o2.cpu().numpy()) < 4e-3 * max(1.0, np.abs(ref["O"]).max())
     if d16:
         monkeypatch.setenv("MFA_DECODE16", "0")
         assert mfa.quantized_plan(desc)[0]["name"].startswith("mfa_fwd_decode_kernel<")

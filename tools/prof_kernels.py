@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Runs one hot-path configuration a few times (a short program for rocprofv3 PMC passes).
-Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv,mla_dec,quant} [reps]"""
+Usage: python tools/prof_kernels.py {c2,c3,c3i8,c5f,c5q,c5kv,mla_dec,quant,dec4,dec8} [reps]"""
 import os
 os.environ.setdefault("MFA_DEV", "1")  # the library reads A/B switches only under MFA_DEV=1
 import sys
@@ -43,6 +43,23 @@ elif which == "mla_dec":
     base = mfa.AttentionDescriptor.make(low_precision=True, precision=mfa.Precision.BF16)
     for _ in range(reps):
         mfa.mla_forward_absorbed(base, lat, wk, wv, q, o, B, H, Sq, Skv, D, LAT, mfa.Precision.BF16)
+elif which in ("dec4", "dec8"):
+    # Split-KV decode as bench.py's int8_decode row (B32 H16 S_kv 8192 D128, S_q 1), INT4 / INT8.
+    B, H, C, D = 32, 16, 8192, 128
+    kv = mfa.Precision.INT4 if which == "dec4" else mfa.Precision.INT8
+    nb = D // 2 if which == "dec4" else D
+    q = u((B, H, 1, D), torch.float16)
+    k = torch.randint(0, 256, (B, H, C, nb), generator=g, device=dev, dtype=torch.uint8)
+    v = torch.randint(0, 256, (B, H, C, nb), generator=g, device=dev, dtype=torch.uint8)
+    o = torch.empty((B, H, 1, D), dtype=torch.float32, device=dev)
+    l = torch.empty((B, H, 1), dtype=torch.float16, device=dev)
+    base = mfa.AttentionDescriptor.make(1, C, D, low_precision=True, precision=mfa.Precision.FP16)
+    qd = mfa.quantized_descriptor(base, mfa.Precision.FP16, kv, kv, B=B, H=H)
+    tq = mfa.quantized_tensor(q, mfa.Precision.FP16)
+    tk = mfa.quantized_tensor(k, kv, scale=0.01)
+    tv = mfa.quantized_tensor(v, kv, scale=0.01)
+    for _ in range(reps):
+        mfa.QuantizedAttention().forward(qd, tq, tk, tv, o, l)
 elif which == "c3i8":
     B, H, S, D = 1, 16, 8192, 128
     qf = u((B, H, S, D), torch.float16)

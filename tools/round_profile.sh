@@ -6,7 +6,7 @@ TAG=${1:-round}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-bash tools/pmc.sh "$TAG/pmc" c2 c3 c3i8 c5f c5q c5kv > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.log"; exit 1; }
+bash tools/pmc.sh "$TAG/pmc" c2 c3 c3i8 c5f c5q c5kv dec4 dec8 > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.log"; exit 1; }
 python3 tools/pmc_traffic.py "$OUT/pmc" > "$OUT/pmc_traffic.json"
 # bench.py reads the newest profiles/r*_pmc_traffic.json for roofline.traffic: this round's.
 cp "$OUT/pmc_traffic.json" "profiles/${TAG}_pmc_traffic.json"
