@@ -154,6 +154,8 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   // Causal: the lane's query index sees keys 0 .. qcol (the host caps C at R, past which no
   // row sees a key).
   const int qcol = rvalid ? row % p.R : 0x3fffffff;
+  // Sliding window (mask row > key + window): the lane's first visible key (host: skip_ok).
+  const int wlo = p.mask.window ? qcol - (int)min(p.mask.window_size, 0x3fffffffu) : -0x40000000;
   {
     const int g = rvalid ? row / p.R : 0, q = rvalid ? row % p.R : 0;
     const int h = kvh + g * p.Hkv;
@@ -282,11 +284,11 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
         sa[0] = E::mma(widen_i8<E>(kb.x, kb.y, zk), qf[st], sa[0]);
       }
     }
-    if (t + BK > p.C || (p.mask.causal && t + BK - 1 > qcol)) {
-      // Keys past C, and (causal) keys past the lane's query index: -inf (key offset
-      // acc_row(r, hh) within the tile).
+    if (t + BK > p.C || (p.mask.causal && t + BK - 1 > qcol) || t < wlo) {
+      // Keys past C, (causal) keys past the lane's query index and (window) keys below
+      // qcol - window: -inf (key offset acc_row(r, hh) within the tile).
       const int last = p.mask.causal ? min(p.C - 1, qcol) : p.C - 1;
-      mask_outside<1>(sa, -0x40000000, last - t - 4 * hh, -__builtin_inff());
+      mask_outside<1>(sa, wlo - t - 4 * hh, last - t - 4 * hh, -__builtin_inff());
     }
     f32x16& s = sa[0];
     float mx = s[0];
@@ -467,6 +469,7 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   const int row = l16;
   const bool rvalid = row < dp.rows;
   const int qcol = rvalid ? row % p.R : 0x3fffffff;
+  const int wlo = p.mask.window ? qcol - (int)min(p.mask.window_size, 0x3fffffffu) : -0x40000000;
   i16x8 qf[NDT];
   {
     const int gq = rvalid ? row / p.R : 0, q = rvalid ? row % p.R : 0;
@@ -588,11 +591,13 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
           sc[kb] = mma16<E>(widen_i8<E>(KC[kb][2 * dt], KC[kb][2 * dt + 1], zk), qf[dt], sc[kb]); \
       }                                                                                          \
     }                                                                                            \
-    if (t + BK > k1 || (p.mask.causal && t + BK - 1 > qcol)) {                                   \
-      const int last = (p.mask.causal ? min(k1 - 1, qcol) : k1 - 1) - t;                         \
+    if (t + BK > k1 || (p.mask.causal && t + BK - 1 > qcol) || t < wlo) {                       \
+      const int last = (p.mask.causal ? min(k1 - 1, qcol) : k1 - 1) - t, first = wlo - t;        \
       _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                         \
-        _Pragma("unroll") for (int e = 0; e < 4; ++e)                                            \
-          sc[kb][e] = 16 * kb + 4 * g + e > last ? -__builtin_inff() : sc[kb][e];                \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                          \
+          const int kk = 16 * kb + 4 * g + e;                                                    \
+          sc[kb][e] = kk > last || kk < first ? -__builtin_inff() : sc[kb][e];                   \
+        }                                                                                        \
     }                                                                                            \
     float mx = fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3]));                      \
     _Pragma("unroll") for (int kb = 1; kb < NKB; ++kb)                                           \

@@ -722,7 +722,9 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
   if (p.k.bscale || p.v.bscale) return false;
   if (p.D % (16 << sh) != 0 || p.D > 256 || p.C <= 0 || !(p.c_log2 > 0.f)) return false;
   // Causal: key <= query index, masked per lane in the kernel; keys past R are never read.
-  if (p.mask.window || p.mask.amask || p.mask.ranges) return false;
+  // Window: keys below query index - window masked per lane (-inf: exact only when no row is
+  // masked everywhere, skip_ok).
+  if (p.mask.amask || p.mask.ranges || (p.mask.window && !p.mask.skip_ok)) return false;
   if (p.q.sd != 1 || !p.q.vec || p.k.sd != 1 || p.v.sd != 1) return false;
   const int64_t al = 16 << sh;
   if (p.k.ss != p.v.ss || p.k.ss % al || p.k.sh % al || p.k.sb % al || p.v.sh % al ||
