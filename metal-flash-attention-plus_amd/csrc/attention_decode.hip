@@ -434,15 +434,18 @@ __device__ __forceinline__ float xgroup_sum(float x) {
 template <int DP, int SRC>
 constexpr int decode16_lds() {
   constexpr int tile = (SRC == SRC_I4 ? 64 * (DP / 2) : 32 * DP);
-  constexpr int ring = 4 * 3 * tile, merge = 4 * 16 * DP * 4 + 4 * 16 * 8;
+  constexpr int ring = 4 * (DP == 256 ? 2 : 3) * tile, merge = 4 * 16 * DP * 4 + 4 * 16 * 8;
   return ring > merge ? ring : merge;
 }
 
 template <class E, int DP, int SRC>
-__global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams dp) {
+__global__ void __launch_bounds__(256, DP == 256 && SRC == SRC_I4 ? 1 : 2)
+    mfa_fwd_decode16_kernel(DecodeParams dp) {
   const FwdParams& p = dp.f;
   constexpr bool I4 = SRC == SRC_I4;
-  constexpr int BK = I4 ? 64 : 32, NKB = BK / 16, NV = 3, NDT = DP / 32, NDB = DP / 16;
+  // V ring slots: 3 (two tiles ahead); 2 at D = 256 (one ahead: two workgroups per CU).
+  constexpr int BK = I4 ? 64 : 32, NKB = BK / 16, NV = DP == 256 ? 2 : 3, NDT = DP / 32;
+  constexpr int NDB = DP / 16;
   constexpr int SH = I4 ? 1 : 0;            // element -> byte offsets
   constexpr int ROWBS = DP >> SH;           // stored bytes per row
   constexpr int TILEBS = BK * ROWBS;        // one stored key tile
@@ -452,7 +455,7 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   constexpr int KLB = ROWBS / 4;            // K bytes per lane per 16-key block
   constexpr int NKL = KLB >= 16 ? KLB / 16 : 1;  // K loads per block (b128, or one b64)
   constexpr int NI = NPV + NKB * NKL;       // vm operations per tile
-  static_assert(DP == 64 || DP == 128, "decode16 widths");
+  static_assert(DP == 64 || DP == 128 || DP == 256, "decode16 widths");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -504,7 +507,9 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   // V chunk swizzle: the 16 (INT4) / 8 + 8 (INT8) rows one transposed read gathers into a
   // 32-lane half spread over the banks (INT4: 2-way at most; INT8: conflict-free).
   auto vsw = [](int r) {
-    if constexpr (I4) return (r >> 4) & (CPR - 1);
+    if constexpr (I4 && CPR == 8) return ((r >> 1) & 1) | (((r >> 4) & 3) << 1);
+    else if constexpr (I4) return (r >> 4) & (CPR - 1);
+    else if constexpr (CPR == 16) return (r & 3) | (((r >> 2) & 1) << 2) | (((r >> 4) & 1) << 3);
     else if constexpr (CPR == 8) return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | (((r >> 4) & 1) << 2);
     else return ((r >> 2) & 1) | (((r >> 4) & 1) << 1);
   };
@@ -566,12 +571,20 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   float m = -kFltMax, lh = 0.f;
 
   // Issue order V(0) K(0) V(1), then per tile i: K(i + 1) V(i + 2): V(i) always precedes K(i),
-  // so one counted vmcnt wait for K(i) covers both.
+  // so one counted vmcnt wait for K(i) covers both.  Two slots (D = 256): K(0) V(0), then per
+  // tile K(i + 1) V(i + 1), and the wait is for V(i).
 #define DEC16_STEP(KC, KN, I)                                                                     \
   {                                                                                              \
     const int ii = (I);                                                                          \
     if (ii + 1 < mine) DEC16_KLOAD(KN, ii + 1);                                                  \
-    if (ii + 2 < mine) {                                                                         \
+    if constexpr (NV == 2) {                                                                     \
+      if (ii + 1 < mine) {                                                                       \
+        vissue(ii + 1);                                                                          \
+        __builtin_amdgcn_s_waitcnt(vm_wait(NI));                                                 \
+      } else {                                                                                   \
+        __builtin_amdgcn_s_waitcnt(vm_wait(0));                                                  \
+      }                                                                                          \
+    } else if (ii + 2 < mine) {                                                                  \
       vissue(ii + 2);                                                                            \
       __builtin_amdgcn_s_waitcnt(vm_wait(NI + NPV));                                             \
     } else if (ii + 1 < mine) {                                                                  \
@@ -640,10 +653,15 @@ __global__ void __launch_bounds__(256, 2) mfa_fwd_decode16_kernel(DecodeParams d
   }
 
   if (mine > 0) {
-    vissue(0);
-    DEC16_KLOAD(ka, 0);
+    if constexpr (NV == 2) {
+      DEC16_KLOAD(ka, 0);
+      vissue(0);
+    } else {
+      vissue(0);
+      DEC16_KLOAD(ka, 0);
+    }
   }
-  if (mine > 1) vissue(1);
+  if (NV == 3 && mine > 1) vissue(1);
   for (int i = 0; i < mine; i += 2) {
     DEC16_STEP(ka, kn, i);
     if (i + 1 < mine) DEC16_STEP(kn, ka, i + 1);
@@ -765,10 +783,11 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
   dp.fused = decode_fused(dp.nsplit);
   if (!dp.fused && !workspace) return hipErrorInvalidValue;
   hipError_t e = hipErrorNotSupported;
-  // At most 16 rows per kv head, D <= 128: the 16x16x32 kernel (MFA_DECODE16=0: the 32-row
-  // one; =4: INT4 only).
+  // At most 16 rows per kv head: the 16x16x32 kernel (MFA_DECODE16=0: the 32-row one; =4: INT4
+  // only; =2: not at D = 256, A/B switches).
   const char* d16 = dev_env("MFA_DECODE16");
-  if (dp.rows <= 16 && DP <= 128 && !(d16 && d16[0] == '0') && (i4 || !(d16 && d16[0] == '4'))) {
+  if (dp.rows <= 16 && !(d16 && d16[0] == '0') && (i4 || !(d16 && d16[0] == '4')) &&
+      !(DP == 256 && d16 && d16[0] == '2')) {
 #define MFA_DEC16(ELEM, EE, DPV)                                                               \
     if (elem == ELEM && DP == DPV)                                                             \
       e = i4 ? launch(mfa_fwd_decode16_kernel<EE, DPV, SRC_I4>, grid, dim3(256),               \
@@ -779,6 +798,8 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
     MFA_DEC16(P_FP16, F16, 128)
     MFA_DEC16(P_BF16, BF16, 64)
     MFA_DEC16(P_BF16, BF16, 128)
+    MFA_DEC16(P_FP16, F16, 256)
+    MFA_DEC16(P_BF16, BF16, 256)
 #undef MFA_DEC16
     if (e != hipSuccess || dp.fused) return e;
     const int64_t nrows = (int64_t)p.B * p.H * p.R;

@@ -522,6 +522,8 @@ def test_integer_matmul_c3_heads(gpu):
     (1, 2, 2, 1, 33, 64, P.FP16),      # one partial tile
     (1, 4, 4, 7, 70, 96, P.BF16),      # D 96 in the 128-wide tiles
     (2, 4, 2, 8, 2500, 128, P.FP16),   # GQA, 16 rows, split path
+    (1, 4, 4, 2, 3000, 256, P.BF16),   # D 256 on the 16-row kernel (INT8)
+    (2, 8, 2, 4, 1500, 256, P.FP16),   # D 256, GQA 16 rows
 ])
 def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     rng = np.random.default_rng(R * 13 + C)
@@ -530,7 +532,7 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
     desc = mfa.quantized_descriptor(base, qp, P.INT8, P.INT8, B=B, H=H, Hkv=Hkv)
     names = [r["name"] for r in mfa.quantized_plan(desc)]
-    d16 = (H // Hkv) * R <= 16 and D <= 128
+    d16 = (H // Hkv) * R <= 16
     assert names[0].startswith("mfa_fwd_decode16_kernel<" if d16 else "mfa_fwd_decode_kernel<"), names
     # One key split per unit: the workgroup merges its waves in LDS (one launch); more
     # splits take the merge pass.
@@ -600,6 +602,7 @@ def test_decode_causal(gpu, kv, B, H, Hkv, R, C, D, qp, monkeypatch):
     (1, 8, 2, 3, 777, 64, 0, P.BF16),       # GQA, window 0: row r sees keys >= r
     (1, 16, 1, 4, 300, 128, 1, P.FP16),     # MQA, two row tiles (the 32-row kernel)
     (2, 2, 2, 40, 60, 256, 10, P.BF16),     # D 256 (the 32-row kernel)
+    (1, 2, 2, 9, 500, 256, 3, P.FP16),      # D 256, 9 rows (INT8: the 16-row kernel)
 ])
 def test_decode_window(gpu, kv, B, H, Hkv, R, C, D, win, qp, monkeypatch):
     rng = np.random.default_rng(R * 41 + C)
@@ -608,7 +611,7 @@ def test_decode_window(gpu, kv, B, H, Hkv, R, C, D, win, qp, monkeypatch):
     base = mfa.AttentionDescriptor.make(R, C, D, window=win, low_precision=True, precision=qp)
     desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
     names = [r["name"] for r in mfa.quantized_plan(desc)]
-    d16 = (H // Hkv) * R <= 16 and D <= 128
+    d16 = (H // Hkv) * R <= 16
     assert names[0].startswith("mfa_fwd_decode16_kernel<" if d16 else "mfa_fwd_decode_kernel<"), names
     o, l, deq, _ = run_qforward(Q, K, V, qp, kv, kv, window=win)
     ref = ol.attention(deq["Q"], deq["K"], deq["V"], window=win)
@@ -630,11 +633,13 @@ def test_decode_window(gpu, kv, B, H, Hkv, R, C, D, win, qp, monkeypatch):
     (1, 2, 2, 16, 4101, 128, P.BF16),  # 16 query rows, partial last tile
     (1, 2, 2, 1, 33, 64, P.FP16),      # one partial 64-key tile
     (1, 4, 4, 7, 70, 96, P.FP16),      # D 96 in the 128-wide tiles
+    (1, 4, 4, 3, 2000, 256, P.BF16),   # D 256 on the 16-row kernel
+    (2, 8, 2, 4, 700, 224, P.FP16),    # D 224 in the 256-wide tiles, GQA 16 rows
 ])
 def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     # INT4 K/V cache at decode shapes on the split-KV kernels: the packed tiles are staged as
     # stored and widened in registers (K by row reads, V^T by 4-bit transposed LDS reads); at
-    # most 16 rows per kv head and D <= 128 take the 16x16x32 kernel.  Held to the oracle on
+    # most 16 rows per kv head take the 16x16x32 kernel.  Held to the oracle on
     # the dequantised values, to the generic dequant-on-load kernel (MFA_DECODE=0) and, for
     # the 16-row kernel, to the 32-row one (MFA_DECODE16=0).
     rng = np.random.default_rng(R * 17 + C)
@@ -643,7 +648,7 @@ def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
     desc = mfa.quantized_descriptor(base, qp, P.INT4, P.INT4, B=B, H=H, Hkv=Hkv)
     names = [r["name"] for r in mfa.quantized_plan(desc)]
-    d16 = (H // Hkv) * R <= 16 and D <= 128
+    d16 = (H // Hkv) * R <= 16
     if d16:
         assert names[0].startswith("mfa_fwd_decode16_kernel<"), names
     else:
