@@ -68,39 +68,41 @@ __device__ __forceinline__ i16x8 i4_order(i16x8 v) {
     return v;
 }
 
-// Combines the np partials (m_s, l_s, O_s) of one query row for columns d .. d+3 and stores
-// O = Σ w_s O_s / (Σ w_s l_s + FLT_MIN), w_s = exp2(m_s - max m), and with write_l also
-// L = max m + log2 l.  Partial s is ml[s·mls] and the D floats at op + s·ops (global memory
-// for the merge pass, LDS for the in-workgroup merge).
-__device__ __forceinline__ void merge_partials(const FwdParams& p, const float2* ml, int64_t mls,
-                                               const float* op, int64_t ops, int np, int b,
-                                               int h, int q, int d, bool write_l) {
-  // Loads in batches of SB partials, all issued before any is used (a one-partial-at-a-time
-  // loop is a chain of memory latencies: the merge pass took as long as the split kernel at
-  // 64 partials per row); the arithmetic is unchanged, partials summed in order.
-  constexpr int SB = 16;
+// Merge of split partials (m_s, l_s, O_s) of one query row, columns d .. d+3:
+// O = Σ w_s O_s / (Σ w_s l_s + FLT_MIN), w_s = exp2(m_s - max m), L = max m + log2 l.  Partial s
+// is ml[s·mls] and the D floats at op + s·ops (global memory for the merge pass, LDS for the
+// in-workgroup merge).  Loads go in batches of SB partials, all issued before any is used (a
+// one-partial-at-a-time loop is a chain of memory latencies: the merge pass took as long as the
+// split kernel at 64 partials per row); partials are summed in order.
+constexpr int kMergeSB = 16;
+
+__device__ __forceinline__ float merge_max(const float2* ml, int64_t mls, int np) {
   float mx = -kFltMax;
-  for (int s0 = 0; s0 < np; s0 += SB) {
-    float mb[SB];
+  for (int s0 = 0; s0 < np; s0 += kMergeSB) {
+    float mb[kMergeSB];
 #pragma unroll
-    for (int u = 0; u < SB; ++u) mb[u] = s0 + u < np ? ml[(s0 + u) * mls].x : -kFltMax;
+    for (int u = 0; u < kMergeSB; ++u) mb[u] = s0 + u < np ? ml[(s0 + u) * mls].x : -kFltMax;
 #pragma unroll
-    for (int u = 0; u < SB; ++u) mx = fmaxf(mx, mb[u]);
+    for (int u = 0; u < kMergeSB; ++u) mx = fmaxf(mx, mb[u]);
   }
-  float l = 0.f;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s0 = 0; s0 < np; s0 += SB) {
-    float2 mlb[SB];
-    float4 vb[SB];
+  return mx;
+}
+
+__device__ __forceinline__ void merge_sum(const FwdParams& p, const float2* ml, int64_t mls,
+                                          const float* op, int64_t ops, int np, float mx, int d,
+                                          float& l, float4& acc) {
+  for (int s0 = 0; s0 < np; s0 += kMergeSB) {
+    float2 mlb[kMergeSB];
+    float4 vb[kMergeSB];
 #pragma unroll
-    for (int u = 0; u < SB; ++u) {
+    for (int u = 0; u < kMergeSB; ++u) {
       const bool in = s0 + u < np;
       mlb[u] = in ? ml[(s0 + u) * mls] : make_float2(-kFltMax, 0.f);
       vb[u] = in && d < p.D ? *reinterpret_cast<const float4*>(op + (s0 + u) * ops + d)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < SB; ++u) {
+    for (int u = 0; u < kMergeSB; ++u) {
       if (s0 + u < np) {
         const float w = __builtin_amdgcn_exp2f(mlb[u].x - mx);
         l += mlb[u].y * w;
@@ -110,6 +112,10 @@ __device__ __forceinline__ void merge_partials(const FwdParams& p, const float2*
       }
     }
   }
+}
+
+__device__ __forceinline__ void merge_store(const FwdParams& p, float4 acc, float l, float mx,
+                                            int b, int h, int q, int d, bool write_l) {
   l += kFltMin;
   const float inv = p.o_mul / l;
   float* orow = p.o + (int64_t)b * p.o_sb + (int64_t)h * p.o_sh + (int64_t)q * p.o_ss;
@@ -125,6 +131,16 @@ __device__ __forceinline__ void merge_partials(const FwdParams& p, const float2*
     else
       reinterpret_cast<float*>(p.l)[li] = L;
   }
+}
+
+__device__ __forceinline__ void merge_partials(const FwdParams& p, const float2* ml, int64_t mls,
+                                               const float* op, int64_t ops, int np, int b,
+                                               int h, int q, int d, bool write_l) {
+  const float mx = merge_max(ml, mls, np);
+  float l = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  merge_sum(p, ml, mls, op, ops, np, mx, d, l, acc);
+  merge_store(p, acc, l, mx, b, h, q, d, write_l);
 }
 
 // s_waitcnt immediate for vmcnt(n) alone (n < 64: bits 3:0 and 15:14).
@@ -752,6 +768,46 @@ __global__ void __launch_bounds__(256) mfa_decode_merge_kernel(DecodeParams dp) 
                  4 * lane, lane == 0);
 }
 
+// Rows with many partials (more than 64: few units, long caches): one row per workgroup, the
+// 4 waves take a quarter of the partials each (the same weights w_s), and their sums meet in
+// LDS.
+__global__ void __launch_bounds__(256) mfa_decode_merge4_kernel(DecodeParams dp) {
+  const FwdParams& p = dp.f;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t rid = blockIdx.x;  // (b·H + h)·R + q
+  const int q = (int)(rid % p.R);
+  const int bh = (int)(rid / p.R);
+  const int h = bh % p.H, b = bh / p.H;
+  const int kvh = h % p.Hkv, g = h / p.Hkv;
+  const int row = g * p.R + q;
+  const int u = (b * p.Hkv + kvh) * dp.nrt + row / 32;
+  const int np = dp.nsplit * 4, nq = np / 4;
+  const int64_t base = ((int64_t)u * np + (int64_t)w * nq) * 32 + (row % 32);
+  const float2* ml = dp.mlpart + base;
+  const float* op = dp.opart + base * p.D;
+  __shared__ float smx[4], sl[4];
+  __shared__ float4 sacc[4][64];
+  const float mw = merge_max(ml, 32, nq);
+  if (lane == 0) smx[w] = mw;
+  __syncthreads();
+  const float mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+  float l = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  merge_sum(p, ml, 32, op, (int64_t)32 * p.D, nq, mx, 4 * lane, l, acc);
+  sacc[w][lane] = acc;
+  if (lane == 0) sl[w] = l;
+  __syncthreads();
+  if (w == 0) {
+    float4 a = sacc[0][lane];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) {
+      const float4 x = sacc[v][lane];
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    }
+    merge_store(p, a, ((sl[0] + sl[1]) + sl[2]) + sl[3], mx, b, h, q, 4 * lane, lane == 0);
+  }
+}
+
 // Keys a decode call reads: all C, or under a causal mask only those some query row sees.
 int decode_keys(int R, int C, bool causal) { return causal ? (C < R ? C : R) : C; }
 
@@ -782,6 +838,15 @@ size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D) {
   if (decode_fused(ns)) return 0;
   const size_t parts = (size_t)B * Hkv * nrt * ns * 4 * 32;
   return parts * D * 4 + parts * 8 + 256;
+}
+
+// The merge pass: one row per wave, or with more than 64 partials per row one row per
+// workgroup (4 waves).
+static hipError_t launch_merge(const DecodeParams& dp, hipStream_t stream) {
+  const int64_t nrows = (int64_t)dp.f.B * dp.f.H * dp.f.R;
+  if (dp.nsplit * 4 > 64)
+    return launch(mfa_decode_merge4_kernel, dim3((unsigned)nrows), dim3(256), 0, stream, dp);
+  return launch(mfa_decode_merge_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, stream, dp);
 }
 
 hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hipStream_t stream) {
@@ -824,8 +889,7 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
     MFA_DEC16(P_BF16, BF16, 256)
 #undef MFA_DEC16
     if (e != hipSuccess || dp.fused) return e;
-    const int64_t nrows = (int64_t)p.B * p.H * p.R;
-    return launch(mfa_decode_merge_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, stream, dp);
+    return launch_merge(dp, stream);
   }
 #define MFA_DEC(ELEM, EE, DPV)                                                                 \
   if (elem == ELEM && DP == DPV)                                                               \
@@ -841,8 +905,7 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
   MFA_DEC(P_BF16, BF16, 256)
 #undef MFA_DEC
   if (e != hipSuccess || dp.fused) return e;
-  const int64_t nrows = (int64_t)p.B * p.H * p.R;
-  return launch(mfa_decode_merge_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, stream, dp);
+  return launch_merge(dp, stream);
 }
 
 }  // namespace mfa

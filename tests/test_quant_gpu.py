@@ -524,6 +524,7 @@ def test_integer_matmul_c3_heads(gpu):
     (2, 4, 2, 8, 2500, 128, P.FP16),   # GQA, 16 rows, split path
     (1, 4, 4, 2, 3000, 256, P.BF16),   # D 256 on the 16-row kernel (INT8)
     (2, 8, 2, 4, 1500, 256, P.FP16),   # D 256, GQA 16 rows
+    (1, 4, 4, 1, 12000, 64, P.FP16),   # 23 splits: 92 partials per row (4-wave merge)
 ])
 def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     rng = np.random.default_rng(R * 13 + C)
@@ -536,7 +537,7 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     assert names[0].startswith("mfa_fwd_decode16_kernel<" if d16 else "mfa_fwd_decode_kernel<"), names
     # One key split per unit: the workgroup merges its waves in LDS (one launch); more
     # splits take the merge pass.
-    assert names[1:] in ([], ["mfa_decode_merge_kernel"]), names
+    assert names[1:] in ([], ["mfa_decode_merge_kernel"], ["mfa_decode_merge4_kernel"]), names
     o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
     ref = ol.attention(deq["Q"], deq["K"], deq["V"])
     assert np.isfinite(o.cpu().numpy()).all()
@@ -635,6 +636,7 @@ def test_decode_window(gpu, kv, B, H, Hkv, R, C, D, win, qp, monkeypatch):
     (1, 4, 4, 7, 70, 96, P.FP16),      # D 96 in the 128-wide tiles
     (1, 4, 4, 3, 2000, 256, P.BF16),   # D 256 on the 16-row kernel
     (2, 8, 2, 4, 700, 224, P.FP16),    # D 224 in the 256-wide tiles, GQA 16 rows
+    (1, 2, 2, 3, 20000, 128, P.BF16),  # 39 splits (4-wave merge)
 ])
 def test_decode_int4(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     # INT4 K/V cache at decode shapes on the split-KV kernels: the packed tiles are staged as
