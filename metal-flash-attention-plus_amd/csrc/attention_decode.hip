@@ -18,9 +18,12 @@
 //     way for O^T += V^T·P^T;
 //   * every wave writes its partial (m, l, unnormalised O) for the valid rows; a merge pass
 //     combines the 4·nsplit partials of each row into O = Σ w_s O_s / Σ w_s l_s and
-//     L = m + log2 l (w_s = exp2(m_s - m)).  With one split per unit (the B32 H16 decode
-//     rows) the workgroup holds all 4 partials and merges them through LDS itself: one
-//     launch, the same arithmetic in the same order.
+//     L = m + log2 l (w_s = exp2(m_s - m)), one row per wave (batched loads), or per 4-wave
+//     workgroup above 64 partials.  With one split per unit (the B32 H16 decode rows) the
+//     workgroup holds all 4 partials and merges them through LDS itself: one launch, the same
+//     arithmetic in the same order.
+// Units with at most 16 rows (the usual decode step) run mfa_fwd_decode16_kernel below: the
+// same layout on 16x16x32 MFMAs, K rows straight from HBM to registers (see its comment).
 #include "mfa_stage.h"
 #include "mfa_dispatch.h"
 
