@@ -332,3 +332,22 @@ def test_decode_bench_shape_is_one_launch():
         base = mfa.AttentionDescriptor.make(R, 8192, 128, low_precision=True, precision=P.FP16)
         desc = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=32, H=16)
         assert [r["name"] for r in mfa.quantized_plan(desc)] == ["mfa_fwd_decode16_kernel<F16, 128, 1>"]
+
+
+def test_decode_kernel_forms():
+    # Split-KV decode routing (attention_decode.hip): at most 16 rows per kv head take the
+    # 16x16x32 kernel at every width, more rows the 32-row kernel; the merge pass runs one row
+    # per wave, or one row per 4-wave workgroup above 64 partials per row.
+    def names(R, C, D, B, H, Hkv, kv, causal=False, window=None):
+        base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, window=window,
+                                            low_precision=True, precision=P.FP16)
+        return [r["name"] for r in mfa.quantized_plan(
+            mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H, Hkv=Hkv))]
+    assert names(1, 16384, 256, 8, 32, 4, P.INT8) == ["mfa_fwd_decode16_kernel<F16, 256, 1>",
+                                                     "mfa_decode_merge_kernel"]
+    assert names(4, 65536, 128, 1, 32, 8, P.INT8) == ["mfa_fwd_decode16_kernel<F16, 128, 1>",
+                                                     "mfa_decode_merge4_kernel"]
+    assert names(1, 8192, 256, 32, 16, 16, P.INT4) == ["mfa_fwd_decode16_kernel<F16, 256, 2>"]
+    assert names(4, 8192, 128, 4, 32, 4, P.INT4)[0] == "mfa_fwd_decode_kernel<F16, 128, 2>"  # 32 rows
+    assert names(16, 4096, 64, 2, 8, 8, P.INT8, causal=True)[0] == "mfa_fwd_decode16_kernel<F16, 64, 1>"
+    assert names(8, 4096, 128, 2, 8, 8, P.INT4, window=64)[0] == "mfa_fwd_decode16_kernel<F16, 128, 2>"
