@@ -16,12 +16,12 @@
 //     (the exact fp16 magic-number conversion of mfa_stage.h); online softmax per wave; V^T
 //     fragments read transposed from the INT8 tile (ds_read_b64_tr_b8) and widened the same
 //     way for O^T += V^T·P^T;
-//   * every wave writes its partial (m, l, unnormalised O) for the valid rows; a merge pass
-//     combines the 4·nsplit partials of each row into O = Σ w_s O_s / Σ w_s l_s and
-//     L = m + log2 l (w_s = exp2(m_s - m)), one row per wave (batched loads), or per 4-wave
-//     workgroup above 64 partials.  With one split per unit (the B32 H16 decode rows) the
-//     workgroup holds all 4 partials and merges them through LDS itself: one launch, the same
-//     arithmetic in the same order.
+//   * the 4 waves' partials (m, l, unnormalised O) meet in LDS; with several key splits the
+//     workgroup writes one combined partial per valid row, and a merge pass combines the
+//     nsplit partials of each row into O = Σ w_s O_s / Σ w_s l_s and L = m + log2 l
+//     (w_s = exp2(m_s - m)), one row per wave (batched loads), or per 4-wave workgroup above
+//     32 splits.  With one split per unit (the B32 H16 decode rows) the workgroup merges its
+//     waves into O and L itself: one launch, the same arithmetic in the same order.
 // Units with at most 16 rows (the usual decode step) run mfa_fwd_decode16_kernel below: the
 // same layout on 16x16x32 MFMAs, K rows straight from HBM to registers (see its comment).
 #include "mfa_stage.h"
@@ -144,6 +144,21 @@ __device__ __forceinline__ void merge_partials(const FwdParams& p, const float2*
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   merge_sum(p, ml, mls, op, ops, np, mx, d, l, acc);
   merge_store(p, acc, l, mx, b, h, q, d, write_l);
+}
+
+// The workgroup's partial of one row (split `split` of unit u) from its 4 waves' partials in
+// LDS: (max m, Σ w l, Σ w O) with the merge's weights and order, columns d .. d+3.
+__device__ __forceinline__ void store_split_partial(const FwdParams& p, const DecodeParams& dp,
+                                                    const float2* ml, int64_t mls,
+                                                    const float* op, int64_t ops, int u,
+                                                    int split, int r, int d) {
+  const float mx = merge_max(ml, mls, 4);
+  float l = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  merge_sum(p, ml, mls, op, ops, 4, mx, d, l, acc);
+  const int64_t pidx = ((int64_t)u * dp.nsplit + split) * 32 + r;
+  if (d < p.D) *reinterpret_cast<float4*>(dp.opart + pidx * p.D + d) = acc;
+  if (d == 0) dp.mlpart[pidx] = make_float2(mx, l);
 }
 
 // s_waitcnt immediate for vmcnt(n) alone (n < 64: bits 3:0 and 15:14).
@@ -385,50 +400,38 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
   }
 
   const float l = cross_half_sum(lh);
-  if (dp.fused) {
-    // One split: the 4 waves' partials meet in LDS ([4][32][DP] O, then [4][32] (m, l)),
-    // over the ring once every wave is done with it, and 256 threads merge them.
-    __syncthreads();
-    float* po = reinterpret_cast<float*>(smem);
-    float2* pml = reinterpret_cast<float2*>(smem + 4 * 32 * DP * 4);
-    float* prow = po + (wave * 32 + l32) * DP;
+  // The 4 waves' partials meet in LDS ([4][32][DP] O, then [4][32] (m, l)) over the ring once
+  // every wave is done with it.  One split: 256 threads merge them into O and L.  Several
+  // splits: they combine them into the workgroup's one partial per row (a quarter of the
+  // partial traffic and merge work of a partial per wave), in the merge's arithmetic, so the
+  // merge pass of a single split reproduces the in-workgroup result bit for bit.
+  __syncthreads();
+  float* po = reinterpret_cast<float*>(smem);
+  float2* pml = reinterpret_cast<float2*>(smem + 4 * 32 * DP * 4);
+  float* prow = po + (wave * 32 + l32) * DP;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(prow + dt * 32 + 8 * g + 4 * hh) =
-            make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
-    if (hh == 0) pml[wave * 32 + l32] = make_float2(m, l);
-    __syncthreads();
-    constexpr int CH = DP / 4, RPI = 256 / CH;  // 16-byte chunks per row, rows per pass
-    const int ch = tid % CH;
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(prow + dt * 32 + 8 * g + 4 * hh) =
+          make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
+  if (hh == 0) pml[wave * 32 + l32] = make_float2(m, l);
+  __syncthreads();
+  constexpr int CH = DP / 4, RPI = 256 / CH;  // 16-byte chunks per row, rows per pass
+  const int ch = tid % CH;
 #pragma unroll
-    for (int k = 0; k < 32 / RPI; ++k) {
-      const int r = tid / CH + k * RPI;
-      const int qr = rt * 32 + r;
-      if (qr < dp.rows) {
+  for (int k = 0; k < 32 / RPI; ++k) {
+    const int r = tid / CH + k * RPI;
+    const int qr = rt * 32 + r;
+    if (qr < dp.rows) {
+      if (dp.fused) {
         const int g = qr / p.R, q = qr % p.R;
         merge_partials(p, pml + r, 32, po + r * DP, 32 * DP, 4, b, kvh + g * p.Hkv, q, 4 * ch,
                        ch == 0);
+      } else {
+        store_split_partial(p, dp, pml + r, 32, po + r * DP, 32 * DP, u, split, r, 4 * ch);
       }
     }
-    return;
-  }
-  // This wave's partial for the tile's valid rows.
-  if (rvalid) {
-    const int np = dp.nsplit * 4;
-    const int64_t pidx = ((int64_t)u * np + split * 4 + wave) * 32 + l32;
-    float* orow = dp.opart + pidx * p.D;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
-        if (d < p.D)
-          *reinterpret_cast<float4*>(orow + d) =
-              make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
-      }
-    if (hh == 0) dp.mlpart[pidx] = make_float2(m, l);
   }
 }
 
@@ -711,48 +714,36 @@ __global__ void __launch_bounds__(256, DP == 256 && SRC == SRC_I4 ? 1 : 2)
 #undef DEC16_KLOAD
 
   const float l = xgroup_sum(lh);
-  if (dp.fused) {
-    // One split: the 4 waves' partials meet in LDS ([4][16][DP] O, then [4][16] (m, l)) over
-    // the ring, and 256 threads merge them.
-    __syncthreads();
-    float* po = reinterpret_cast<float*>(smem);
-    float2* pml = reinterpret_cast<float2*>(smem + 4 * 16 * DP * 4);
-    float* prow = po + (wave * 16 + l16) * DP;
+  // The 4 waves' partials meet in LDS ([4][16][DP] O, then [4][16] (m, l)) over the ring; one
+  // split: 256 threads merge them; several: the workgroup's one partial per row (as above).
+  __syncthreads();
+  float* po = reinterpret_cast<float*>(smem);
+  float2* pml = reinterpret_cast<float2*>(smem + 4 * 16 * DP * 4);
+  float* prow = po + (wave * 16 + l16) * DP;
 #pragma unroll
-    for (int db = 0; db < NDB; ++db)
-      *reinterpret_cast<float4*>(prow + 16 * db + 4 * g) =
-          make_float4(o[db][0], o[db][1], o[db][2], o[db][3]);
-    if (g == 0) pml[wave * 16 + l16] = make_float2(m, l);
-    __syncthreads();
-    constexpr int CH = DP / 4, RPI = 256 / CH;  // 16-byte chunks per row, rows per pass
-    const int ch = tid % CH;
+  for (int db = 0; db < NDB; ++db)
+    *reinterpret_cast<float4*>(prow + 16 * db + 4 * g) =
+        make_float4(o[db][0], o[db][1], o[db][2], o[db][3]);
+  if (g == 0) pml[wave * 16 + l16] = make_float2(m, l);
+  __syncthreads();
+  constexpr int CH = DP / 4, RPI = 256 / CH;  // 16-byte chunks per row, rows per pass
+  const int ch = tid % CH;
 #pragma unroll
-    for (int k = 0; k < 16 / RPI; ++k) {
-      const int r = tid / CH + k * RPI;
-      if (r < dp.rows) {
+  for (int k = 0; k < 16 / RPI; ++k) {
+    const int r = tid / CH + k * RPI;
+    if (r < dp.rows) {
+      if (dp.fused) {
         const int gq = r / p.R, q = r % p.R;
         merge_partials(p, pml + r, 16, po + r * DP, 16 * DP, 4, b, kvh + gq * p.Hkv, q, 4 * ch,
                        ch == 0);
+      } else {
+        store_split_partial(p, dp, pml + r, 16, po + r * DP, 16 * DP, u, split, r, 4 * ch);
       }
     }
-    return;
-  }
-  // This wave's partial for the valid rows (the 32-row partial layout of the merge pass).
-  if (rvalid) {
-    const int np = dp.nsplit * 4;
-    const int64_t pidx = ((int64_t)u * np + split * 4 + wave) * 32 + l16;
-    float* orow = dp.opart + pidx * p.D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db) {
-      const int d = 16 * db + 4 * g;
-      if (d < p.D)
-        *reinterpret_cast<float4*>(orow + d) = make_float4(o[db][0], o[db][1], o[db][2], o[db][3]);
-    }
-    if (g == 0) dp.mlpart[pidx] = make_float2(m, l);
   }
 }
 
-// One query row per wave: combines the row's 4·nsplit partials.  O is written with the
+// One query row per wave: combines the row's nsplit partials.  O is written with the
 // caller's strides, L = m + log2 l in the descriptor's memory precision.
 __global__ void __launch_bounds__(256) mfa_decode_merge_kernel(DecodeParams dp) {
   const FwdParams& p = dp.f;
@@ -765,13 +756,13 @@ __global__ void __launch_bounds__(256) mfa_decode_merge_kernel(DecodeParams dp) 
   const int kvh = h % p.Hkv, g = h / p.Hkv;
   const int row = g * p.R + q;
   const int u = (b * p.Hkv + kvh) * dp.nrt + row / 32;
-  const int np = dp.nsplit * 4;
+  const int np = dp.nsplit;  // one partial per split (the workgroup's)
   const int64_t base = (int64_t)u * np * 32 + (row % 32);
   merge_partials(p, dp.mlpart + base, 32, dp.opart + base * p.D, (int64_t)32 * p.D, np, b, h, q,
                  4 * lane, lane == 0);
 }
 
-// Rows with many partials (more than 64: few units, long caches): one row per workgroup, the
+// Rows with many partials (more than 32: few units, long caches): one row per workgroup, the
 // 4 waves take a quarter of the partials each (the same weights w_s), and their sums meet in
 // LDS.
 __global__ void __launch_bounds__(256) mfa_decode_merge4_kernel(DecodeParams dp) {
@@ -784,8 +775,8 @@ __global__ void __launch_bounds__(256) mfa_decode_merge4_kernel(DecodeParams dp)
   const int kvh = h % p.Hkv, g = h / p.Hkv;
   const int row = g * p.R + q;
   const int u = (b * p.Hkv + kvh) * dp.nrt + row / 32;
-  const int np = dp.nsplit * 4, nq = np / 4;
-  const int64_t base = ((int64_t)u * np + (int64_t)w * nq) * 32 + (row % 32);
+  const int np = dp.nsplit, s0 = w * np / 4, nq = (w + 1) * np / 4 - s0;
+  const int64_t base = ((int64_t)u * np + s0) * 32 + (row % 32);
   const float2* ml = dp.mlpart + base;
   const float* op = dp.opart + base * p.D;
   __shared__ float smx[4], sl[4];
@@ -839,15 +830,15 @@ size_t decode_workspace_bytes(int B, int Hkv, int rows, int C, int D) {
   int nrt, ns, chunk;
   decode_layout(B, Hkv, rows, C, &nrt, &ns, &chunk);
   if (decode_fused(ns)) return 0;
-  const size_t parts = (size_t)B * Hkv * nrt * ns * 4 * 32;
+  const size_t parts = (size_t)B * Hkv * nrt * ns * 32;  // one partial per split and row
   return parts * D * 4 + parts * 8 + 256;
 }
 
-// The merge pass: one row per wave, or with more than 64 partials per row one row per
+// The merge pass: one row per wave, or with more than 32 partials (splits) per row one row per
 // workgroup (4 waves).
 static hipError_t launch_merge(const DecodeParams& dp, hipStream_t stream) {
   const int64_t nrows = (int64_t)dp.f.B * dp.f.H * dp.f.R;
-  if (dp.nsplit * 4 > 64)
+  if (dp.nsplit > 32)
     return launch(mfa_decode_merge4_kernel, dim3((unsigned)nrows), dim3(256), 0, stream, dp);
   return launch(mfa_decode_merge_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, stream, dp);
 }
@@ -862,7 +853,7 @@ hipError_t fwd_decode_dispatch(const FwdParams& p, int elem, void* workspace, hi
   if (p.mask.causal) dp.f.C = decode_keys(p.R, p.C, true);
   dp.rows = (p.H / p.Hkv) * p.R;
   decode_layout(p.B, p.Hkv, dp.rows, dp.f.C, &dp.nrt, &dp.nsplit, &dp.chunk);
-  const size_t parts = (size_t)p.B * p.Hkv * dp.nrt * dp.nsplit * 4 * 32;
+  const size_t parts = (size_t)p.B * p.Hkv * dp.nrt * dp.nsplit * 32;
   dp.opart = (float*)workspace;
   dp.mlpart = workspace ? (float2*)((char*)workspace + ((parts * p.D * 4 + 255) & ~(size_t)255))
                         : nullptr;

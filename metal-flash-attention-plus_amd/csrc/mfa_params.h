@@ -83,8 +83,8 @@ struct DecodeParams {
   int32_t nrt;       // 32-row tiles per kv head
   int32_t nsplit;    // key splits per unit (unit = batch, kv head, row tile)
   int32_t chunk;     // keys per split (whole rounds of 4 waves x 32-key tiles)
-  float* opart;      // [units][4·nsplit][32][D] unnormalised O of each wave
-  float2* mlpart;    // [units][4·nsplit][32] (m, l)
+  float* opart;      // [units][nsplit][32][D] unnormalised O of each workgroup (its 4 waves combined)
+  float2* mlpart;    // [units][nsplit][32] (m, l)
   int32_t fused;     // nsplit == 1: the workgroup merges its 4 waves' partials in LDS
 };
 

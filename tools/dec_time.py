@@ -17,6 +17,9 @@ st = torch.cuda.Stream()
 g = torch.Generator(device=dev).manual_seed(5)
 cases = [(8, 32, 4, 1, 16384, 256, 8), (8, 32, 8, 1, 16384, 128, 4), (4, 32, 8, 1, 32768, 128, 8),
          (1, 32, 8, 4, 65536, 128, 8), (32, 16, 16, 1, 8192, 128, 8)]
+if os.environ.get("DEC_SET") == "rows":  # more than 16 rows per kv head (the 32-row kernel)
+    cases = [(8, 32, 4, 4, 16384, 128, 8), (8, 32, 4, 4, 16384, 128, 4), (8, 64, 8, 4, 16384, 128, 8),
+             (8, 32, 4, 8, 16384, 128, 8), (32, 32, 8, 4, 4096, 128, 8)]
 out = []
 for B, H, Hkv, R, C, D, bits in cases:
     kv = P.INT8 if bits == 8 else P.INT4
