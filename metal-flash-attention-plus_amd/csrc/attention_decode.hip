@@ -437,7 +437,8 @@ __global__ void __launch_bounds__(256, DP >= 256 ? 1 : 2) mfa_fwd_decode_kernel(
 
 // ---------------------------------------------------------------------------------------
 // At most 16 query rows per kv head (the usual decode step: S_q 1-16, GQA groups up to 16
-// rows), D <= 128: the same split / partial / merge layout on v_mfma_f32_16x16x32, whose
+// rows), D <= 256 (INT4 at D = 256 at one wave per SIMD): the same split / partial / merge
+// layout on v_mfma_f32_16x16x32, whose
 // 16-query output halves the per-key softmax work of the 32-row tile (a lane holds one score
 // per 4 keys instead of per 2) and whose K operand rows are contiguous reads:
 //   * key tiles of BK = 64 (INT4) / 32 (INT8), each wave its own; K goes from HBM straight to

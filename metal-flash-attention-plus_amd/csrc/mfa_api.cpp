@@ -128,13 +128,20 @@ mfa_status_t scratch(size_t bytes, void** out, int slot, hipStream_t stream, siz
     b.ptr = p;
     b.bytes = bytes;
   }
-  if (zero_bytes > b.zeroed) {
+  // Under stream capture the memset is only recorded into the graph, not run: a captured call
+  // always records its own memset (the graph may replay after eager calls that left partial
+  // states in its counter region), and afterwards no prefix is known to be zero, so the next
+  // eager call on this stream zeroes again.
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  const bool capturing =
+      hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+  if (zero_bytes > b.zeroed || (capturing && zero_bytes > 0)) {
     const hipError_t e = hipMemsetAsync(b.ptr, 0, zero_bytes, stream);
     if (e != hipSuccess) return hip_status(e, "hipMemsetAsync(scratch)");
   }
   // After this call's launch only its own counter prefix is known to be zero again: the bytes
   // behind it hold this call's partial states.
-  b.zeroed = zero_bytes;
+  b.zeroed = capturing ? 0 : zero_bytes;
   *out = b.ptr;
   return MFA_SUCCESS;
 }

@@ -186,3 +186,54 @@ def test_stream_workspace_counter_region_grows(gpu):
     mfa.MultiHeadAttention().forward(desc, q, k, v, o, l)
     torch.cuda.synchronize()
     assert torch.equal(o, o1) and torch.equal(l, l1)
+
+
+def test_stream_workspace_zeroing_under_graph_capture(gpu):
+    # a call captured into a HIP graph only records its workspace memset.  An eager
+    # call on the same stream between the capture and the replay must still zero the counter
+    # region, which the eager call before the capture (a shorter counter prefix) filled with
+    # partial states.  Order: eager long-prefix (B8 D64), eager short-prefix (B4 D128, leaves
+    # partial states behind its 4 KiB of counters), capture the long-prefix call, then the
+    # long-prefix call eagerly, the graph replayed, and the eager call again: every result equal
+    # to the first one bit for bit.
+    H, S = 16, 4096
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    st = torch.cuda.Stream()
+    mha = mfa.MultiHeadAttention()
+
+    def problem(B, D):
+        q, k, v = ((torch.rand((B, H, S, D), generator=g, device="cuda:0") * 2 - 1).half()
+                   for _ in range(3))
+        base = mfa.AttentionDescriptor.make(low_precision=True, precision=FP16, causal=True)
+        desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
+        o = torch.empty((B, H, S, D), dtype=torch.float32, device="cuda:0")
+        l = torch.empty((B, H, S), dtype=torch.float16, device="cuda:0")
+        return desc, q, k, v, o, l
+
+    long_p, short_p = problem(8, 64), problem(4, 128)
+    torch.cuda.synchronize()
+
+    def run(pr):
+        desc, q, k, v, o, l = pr
+        mha.forward(desc, q, k, v, o, l, stream=st.cuda_stream)
+
+    with torch.cuda.stream(st):
+        mfa.last_launches()
+        run(long_p)
+        st.synchronize()
+        assert launched()[-1].startswith("mfa_fwd2_stream_kernel"), launched()
+        ref_o, ref_l = long_p[4].clone(), long_p[5].clone()
+        _torch_ref_check(*long_p[1:4], ref_o, ref_l, ((0, 0), (7, 15)), 5e-3)
+        run(short_p)
+        st.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=st):
+            run(long_p)
+        for phase in ("eager", "replay", "eager again"):
+            long_p[4].fill_(float("nan"))
+            if phase == "replay":
+                graph.replay()
+            else:
+                run(long_p)
+            st.synchronize()
+            assert torch.equal(long_p[4], ref_o) and torch.equal(long_p[5], ref_l), phase

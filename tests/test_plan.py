@@ -96,7 +96,7 @@ def test_misaligned_query_falls_back_to_generic_kernel():
 def test_quantized_plans():
     base = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.FP16)
     qi = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, integer_matmul=True)
-    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 128, 2, 2>"
+    assert one(mfa.quantized_plan(qi))["name"] == "mfa_fwd_i8_kernel<F16, 128, 128, 2, 2, true>"
     # Dequant-exact forward, FP16 Q + per-tensor INT8 K/V: one kernel widening the bytes as
     # it stages them (attention_fwd_kv8.hip), no pass.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
@@ -337,7 +337,7 @@ def test_decode_bench_shape_is_one_launch():
 def test_decode_kernel_forms():
     # Split-KV decode routing (attention_decode.hip): at most 16 rows per kv head take the
     # 16x16x32 kernel at every width, more rows the 32-row kernel; the merge pass runs one row
-    # per wave, or one row per 4-wave workgroup above 64 partials per row.
+    # per wave, or one row per 4-wave workgroup above 32 partials (key splits) per row.
     def names(R, C, D, B, H, Hkv, kv, causal=False, window=None):
         base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, window=window,
                                             low_precision=True, precision=P.FP16)

@@ -368,14 +368,30 @@ def test_quantized_backward_on_fast_kernels(gpu, kv, D, zps, S, monkeypatch):
     oracle on the dequantised values, and (S = 300) give dQ bit for bit as the pass + 16-bit
     kernel path (the default there: the same kernel on the dense copy, the same MFMA
     operands)."""
-    B, H = 1, 2
-    if S >= 128:
+    _quantized_backward_fast(kv, D, zps, S, monkeypatch)
+
+
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("D,H,Hkv,S,window", [(128, 8, 2, 100, None), (64, 4, 1, 60, None),
+                                               (128, 2, 2, 300, 96), (256, 8, 2, 40, 24),
+                                               (64, 6, 3, 200, 50)])
+def test_quantized_backward_bytes_gqa_window(gpu, kv, D, H, Hkv, S, window, monkeypatch):
+    """the byte-ring backwardQuery with GQA / MQA head mapping (kv head = h % Hkv
+    of the group) and sliding windows (in place of the causal pattern), held to the oracle and (at >= 128 query rows per
+    kv head, where the pass is the default) bit for bit to the pass path."""
+    _quantized_backward_fast(kv, D, (2, -3), S, monkeypatch, H=H, Hkv=Hkv, window=window)
+
+
+def _quantized_backward_fast(kv, D, zps, S, monkeypatch, H=2, Hkv=2, window=None):
+    B = 1
+    rows_per_kv = (H // Hkv) * S
+    if rows_per_kv >= 128:
         monkeypatch.setenv("MFA_BWDQ_BYTES", "1")
-    rng = np.random.default_rng(23 + D)
-    Q, K, V, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) * 0.5 for _ in range(4))
+    rng = np.random.default_rng(23 + D + 7 * H + Hkv + S)
+    Q, dO = (rng.standard_normal((B, H, S, D)).astype(np.float32) * 0.5 for _ in range(2))
     lim = 120 if kv == P.INT8 else 8
-    kq8 = rng.integers(-lim, lim, (B, H, S, D)).astype(np.int8)
-    vq8 = rng.integers(-lim, lim, (B, H, S, D)).astype(np.int8)
+    kq8 = rng.integers(-lim, lim, (B, Hkv, S, D)).astype(np.int8)
+    vq8 = rng.integers(-lim, lim, (B, Hkv, S, D)).astype(np.int8)
     ks, vs = 0.004 if kv == P.INT8 else 0.06, 0.005 if kv == P.INT8 else 0.07
     kd = ((kq8.astype(np.float32) - zps[0]) * np.float32(ks)).astype(np.float32)
     vd = ((vq8.astype(np.float32) - zps[1]) * np.float32(vs)).astype(np.float32)
@@ -385,10 +401,11 @@ def test_quantized_backward_on_fast_kernels(gpu, kv, D, zps, S, monkeypatch):
         pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
         kt, vt = tdev(pack(kq8.astype(np.int32)), torch.uint8), tdev(pack(vq8.astype(np.int32)), torch.uint8)
     Qd, dOd = seen(Q, P.FP16), seen(dO, P.FP16)
-    ref = ol.attention(Qd, kd, vd, dO=dOd, causal=True)
-    base = mfa.AttentionDescriptor.make(S, S, D, causal=True, low_precision=True,
+    # (A sliding window replaces the causal pattern: AttentionDescriptor.sparsityPattern holds one.)
+    ref = ol.attention(Qd, kd, vd, dO=dOd, causal=window is None, window=window)
+    base = mfa.AttentionDescriptor.make(S, S, D, causal=True, window=window, low_precision=True,
                                         precision=P.FP16)
-    desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H)
+    desc = mfa.quantized_descriptor(base, P.FP16, kv, kv, B=B, H=H, Hkv=Hkv)
     tq = mfa.quantized_tensor(to_device(Q, P.FP16), P.FP16)
     tk = mfa.quantized_tensor(kt, kv, scale=ks, zero_point=zps[0])
     tv = mfa.quantized_tensor(vt, kv, scale=vs, zero_point=zps[1])
@@ -400,7 +417,8 @@ def test_quantized_backward_on_fast_kernels(gpu, kv, D, zps, S, monkeypatch):
 
     def run():
         dq = torch.full((B, H, S, D), float("nan"), dtype=torch.float32, device=DEV)
-        dk, dv = torch.empty_like(dq), torch.empty_like(dq)
+        dk = torch.empty((B, Hkv, S, D), dtype=torch.float32, device=DEV)
+        dv = torch.empty_like(dk)
         dvals = torch.empty((B, H, S), dtype=torch.bfloat16, device=DEV)
         plan = (mfa.quantized_plan(desc, mfa.KernelType.backwardQuery, tq, tk, tv) +
                 mfa.quantized_plan(desc, mfa.KernelType.backwardKeyValue, tq, tk, tv))
@@ -416,7 +434,7 @@ def test_quantized_backward_on_fast_kernels(gpu, kv, D, zps, S, monkeypatch):
                      f"mfa_bwd_kv_fast_kernel<F16, {D}, {32 if D == 256 else 64}, {src}, false>"], names
     for name, t in (("dQ", dq), ("dK", dk), ("dV", dv)):
         assert maxerr(t, ref[name]) < 5e-2 * max(1.0, np.abs(ref[name]).max()), name
-    if S < 128:
+    if rows_per_kv < 128:
         return
     monkeypatch.delenv("MFA_BWDQ_BYTES")
     names2, dq2, _, _, dvals2 = run()
@@ -524,7 +542,8 @@ def test_integer_matmul_c3_heads(gpu):
     (2, 4, 2, 8, 2500, 128, P.FP16),   # GQA, 16 rows, split path
     (1, 4, 4, 2, 3000, 256, P.BF16),   # D 256 on the 16-row kernel (INT8)
     (2, 8, 2, 4, 1500, 256, P.FP16),   # D 256, GQA 16 rows
-    (1, 4, 4, 1, 12000, 64, P.FP16),   # 23 splits: 92 partials per row (4-wave merge)
+    (1, 4, 4, 1, 12000, 64, P.FP16),   # 23 splits: the one-wave merge pass
+    (1, 2, 2, 1, 24000, 64, P.FP16),   # 38 splits (> 32 partials per row): the 4-wave merge
 ])
 def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     rng = np.random.default_rng(R * 13 + C)
@@ -538,6 +557,10 @@ def test_decode_split_kv(gpu, B, H, Hkv, R, C, D, qp, monkeypatch):
     # One key split per unit: the workgroup merges its waves in LDS (one launch); more
     # splits take the merge pass.
     assert names[1:] in ([], ["mfa_decode_merge_kernel"], ["mfa_decode_merge4_kernel"]), names
+    if C == 24000:
+        assert names[1:] == ["mfa_decode_merge4_kernel"], names
+    elif C == 12000:
+        assert names[1:] == ["mfa_decode_merge_kernel"], names
     o, l, deq, _ = run_qforward(Q, K, V, qp, P.INT8, P.INT8)
     ref = ol.attention(deq["Q"], deq["K"], deq["V"])
     assert np.isfinite(o.cpu().numpy()).all()
