@@ -40,7 +40,13 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 // NG = 2 (unmasked forwards): a 512-thread workgroup of two 4-wave groups owns the adjacent
 // 128-row blocks (2·pi, 2·pi + 1), and every K/V tile, staged by all 8 waves, serves both
 // (256 query rows per staged tile, half the LDS-DMA of two 4-wave workgroups).
-template <class E, int DP, int BK, int OCC, int NG = 1>
+// BIAS (round 6): the QK^T chains start from a register tile holding the bits of 1.5 * 2^23
+// (0x4B400000) instead of 0, so each INT32 score S comes out as the FP32 bit pattern of
+// 1.5 * 2^23 + S (|S| <= 127 * 127 * 128 < 2^22 keeps it in one binade): no int -> float
+// conversion per score.  The bias is taken out of the row max by one exact subtraction per row
+// and folded into the exp2 argument's constant (fma(1.5 * 2^23 + S, c, -(1.5 * 2^23 c + m'))),
+// so the per-score VALU is max, fma, exp2, add, byte pack.
+template <class E, int DP, int BK, int OCC, int NG = 1, bool BIAS = true>
 __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) {
   static_assert(DP == 128 && (BK == 64 || BK == 128), "int8 kernel: D<=128, 64/128-key tiles");
   using TK = Tile16<DP / 2>;            // [BK][DP bytes] = 16-byte chunks, DP/16 per row
@@ -163,6 +169,10 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
   }
   __syncthreads();
 
+  constexpr float kBias = 12582912.0f;  // 1.5 * 2^23, bits 0x4B400000
+  i32x16 bias0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bias0[i] = BIAS ? 0x4B400000 : 0;
   int cur = 0;
   for (int t = kbeg; t < kend; t += BK) {
     const bool has_next = t + BK < kend;
@@ -174,10 +184,6 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
     const char* vt = vb0 + cur * VTILE;
 
     i32x16 si[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) si[j][i] = 0;
     {
       // K fragments read AH MFMAs ahead; sched_barrier(0) pins the order.
       constexpr int NM = KSTEPS * NJ, AH = 4;
@@ -188,7 +194,8 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
 #pragma unroll
       for (int i = 0; i < NM; ++i) {
         const int j = i % NJ;
-        si[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(kf[i % AH], qf[i / NJ], si[j], 0, 0, 0);
+        si[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(kf[i % AH], qf[i / NJ], i < NJ ? bias0 : si[j],
+                                                      0, 0, 0);
         if (i + AH < NM) {
           const int n = i + AH;
           kf[i % AH] = *reinterpret_cast<const i32x4*>(kt + TK::off((n % NJ) * 32 + l32, 2 * (n / NJ) + hh));
@@ -199,9 +206,13 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
 
     float sf[NJ][16];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      // (The whole vector is bit-cast: hipcc 7.2 folds __builtin_bit_cast(float, v[i]) of an
+      // element of an MFMA result vector to element 0 for every i.)
+      const f32x16 fj = __builtin_bit_cast(f32x16, si[j]);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sf[j][i] = (float)si[j][i];
+      for (int i = 0; i < 16; ++i) sf[j][i] = BIAS ? fj[i] : (float)si[j][i];
+    }
     const bool edge = t + BK > p.C;
     const bool diag = p.mask.causal && t + BK - 1 > q0;
     if (edge || diag || p.mask.window) {
@@ -220,7 +231,7 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sf[j][i]);
-    const float m_tile = xh_max(mx) * cq;
+    const float m_tile = (BIAS ? xh_max(mx) - kBias : xh_max(mx)) * cq;  // exact subtraction
     // The running max is kept integer-valued (rounded up), so a rescale multiplies O_int by
     // an exact power of two: one arithmetic shift per accumulator instead of a float round
     // trip.  P' keeps at least 6 of its 7 bits (the rounded max exceeds the true one by < 1).
@@ -239,7 +250,10 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
     }
     // P' = 127 P = exp2(s*c - (m - log2 127)) in [0, 127]; v_cvt_pk_u8_f32 rounds it into
     // byte e of the packed B operand.  l accumulates P' (the 127 cancels in O = Σ P'v / Σ P').
-    const float mq = m - 6.98868468677217f;  // log2(127)
+    // (BIAS: the exp2 argument's constant also takes out 1.5 * 2^23 * c; for a row at the mask
+    // level m is so large that the bias vanishes in it and the exact path below is unchanged.)
+    const float mq = BIAS ? __builtin_fmaf(kBias, cq, m - 6.98868468677217f)
+                          : m - 6.98868468677217f;  // log2(127)
     float (&ps)[NJ][16] = sf;
     if (__any(m < kMaskLevel)) {
 #pragma unroll
@@ -346,13 +360,13 @@ __global__ void __launch_bounds__(256 * NG, OCC) mfa_fwd_i8_kernel(FwdParams p) 
   }
 }
 
-template <class E, int BK, int OCC, int NG = 1>
+template <class E, int BK, int OCC, int NG = 1, bool BIAS = true>
 static hipError_t launch_i8(const FwdParams& p, hipStream_t stream) {
   // K and V double-buffered; two groups: also the O row images of the epilogue.
   constexpr int RING = 4 * BK * 128, OIMG = NG * 128 * (128 * 4 + 16);
   constexpr int LDS = NG == 2 && OIMG > RING ? OIMG : RING;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = mfa_fwd_i8_kernel<E, 128, BK, OCC, NG>;
+  auto kern = mfa_fwd_i8_kernel<E, 128, BK, OCC, NG, BIAS>;
   const int units = (p.nblk + NG - 1) / NG;
   return launch(kern, dim3(units * p.B * p.H), dim3(256 * NG), LDS, stream, p);
 }
@@ -370,6 +384,11 @@ hipError_t fwd_i8mma_dispatch(const FwdParams& p, int elem, hipStream_t stream) 
   if (!small && !p.mask.causal && !p.mask.window &&
       (sh ? sh[0] == '1'
           : (p.nblk % 2 == 0 || p.nblk >= 8) && (int64_t)((p.nblk + 1) / 2) * p.B * p.H >= 256)) {
+    const char* bz = mfa::dev_env("MFA_I8_BIAS");  // =0: the converted-score kernel (A/B)
+    if (bz && bz[0] == '0') {
+      if (elem == P_FP16) return launch_i8<F16, 128, 2, 2, false>(p, stream);
+      if (elem == P_BF16) return launch_i8<BF16, 128, 2, 2, false>(p, stream);
+    }
     if (elem == P_FP16) return launch_i8<F16, 128, 2, 2>(p, stream);
     if (elem == P_BF16) return launch_i8<BF16, 128, 2, 2>(p, stream);
   }
@@ -386,5 +405,7 @@ template __global__ void mfa_fwd_i8_kernel<F16, 128, 128, 2>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<BF16, 128, 128, 2>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<F16, 128, 128, 2, 2>(FwdParams);
 template __global__ void mfa_fwd_i8_kernel<BF16, 128, 128, 2, 2>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<F16, 128, 128, 2, 2, false>(FwdParams);
+template __global__ void mfa_fwd_i8_kernel<BF16, 128, 128, 2, 2, false>(FwdParams);
 
 }  // namespace mfa
