@@ -507,6 +507,11 @@ __device__ __forceinline__ void fwd2_share_body(const FwdParams& p) {
   const int wsz = 0x3fffffff;
   MFA_STAMP(0);
   MFA_CYC(0);
+  if (MIRROR && pi >= p.pro_split) {
+    // Light pairs: the heavy pairs' prologue (Q of both blocks, the first tiles: every CU at
+    // once, HBM-bound) goes first.
+    for (int i = 0; i < p.pro_delay; ++i) __builtin_amdgcn_s_sleep(8);
+  }
 
   DmaA<DP, BK, NT> kd, vd;         // a group's own tiles
   DmaA<DP, BK, 2 * NT> ksh, vsh;   // shared tiles, staged by all 8 waves
@@ -716,7 +721,13 @@ __device__ __forceinline__ void fwd2_share_body(const FwdParams& p) {
       vsh.issue(vhead, b0 + (s + 1) * BK, sv + nx * TILEB);
     } else {
       int tn;
+#ifdef MFA_ABLATE_P2_DMA
+      // Diagnostic builds only (tools/diag/fwd_stamps_p2): phase 2 computes on whatever its
+      // ring holds, to price its own-tile staging.  Results are wrong.
+      if (s + 1 == nA && tile(s + 1, tn)) {
+#else
       if (tile(s + 1, tn)) {
+#endif
         kd.issue(khead, tn, kb0 + nx * TILEB);
         vd.issue(vhead, tn, vb0 + nx * TILEB);
       }
@@ -974,6 +985,18 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   {
     const char* xh = mfa::dev_env("MFA_SHARE_XCD");  // A/B: 0 deals pairs round-robin over heads
     q.xcd_heads = !(xh && xh[0] == '0');
+  }
+  {
+    // Mirrored pairs: the light half of the pairs waits 8 x 512 cycles (~2 us) before its
+    // prologue loads, so the heavy pairs (the critical path: ~7 us more loop than the lightest)
+    // get the prologue's HBM burst first.  C2, one-process A/B over delays 0/4/8/12 and splits
+    // 4/8/12 (profiles/r06d_ab_prologue_delay.txt): 0.0733 -> 0.0721 ms at split 8 (+1.7 %),
+    // +0.4..0.7 % in the other two runs.  A/B knobs: MFA_FWD_DELAY (rounds),
+    // MFA_FWD_DELAY_SPLIT (first delayed pair index).
+    const char* dl = mfa::dev_env("MFA_FWD_DELAY");
+    const char* ds = mfa::dev_env("MFA_FWD_DELAY_SPLIT");
+    q.pro_delay = dl ? atoi(dl) : 8;
+    q.pro_split = ds ? atoi(ds) : npairs / 2;
   }
   // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
   // (A/B).

@@ -52,6 +52,10 @@ struct FwdParams {
   int32_t sk_len, sk_total, sk_head, sk_cnt_bytes;
   int32_t sk_flags;        // bit 0: closers always publish (tests)
   int32_t xcd_heads;       // adjacent shared-tile pairs: a head's pairs together on one XCD
+  // Mirrored causal pairs: the light pairs (pair index >= pro_split) wait pro_delay rounds of
+  // 512 shader cycles before their prologue loads, so the heavy pairs' prologue burst (the
+  // kernel's critical path) has HBM to itself.
+  int32_t pro_delay, pro_split;
 };
 
 struct BwdParams {

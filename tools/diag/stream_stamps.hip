@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
   const int S = argc > 2 ? atoi(argv[2]) : 4096;
   const int D = argc > 3 ? atoi(argv[3]) : 128;
   if (argc > 4) setenv("MFA_FWD_STREAM_WGS", argv[4], 1);
+  setenv("MFA_DEV", "1", 1);  // the library reads its A/B switches only under MFA_DEV=1
   setenv("MFA_FWD_STREAM", "1", 1);
   const int B = 1;
   const size_t n = (size_t)B * H * S * D;
