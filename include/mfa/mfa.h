@@ -44,7 +44,12 @@ typedef enum mfa_status {
   MFA_ERR_UNSUPPORTED = 2,        /* configuration the kernels do not implement */
   MFA_ERR_LAUNCH = 3,             /* hipLaunchKernel / runtime failure */
   MFA_ERR_INVALID_ARGUMENT = 4,   /* null pointer / bad size */
-  MFA_ERR_NO_DEVICE = 5
+  MFA_ERR_NO_DEVICE = 5,
+  /* Range sentinels (never valid values): the enum spans every int32, so a value a binding
+     passes from outside the list is range-checked by the library instead of being
+     undefined behaviour in C++. */
+  MFA_STATUS_RANGE_MIN_ = -0x7fffffff - 1,
+  MFA_STATUS_RANGE_MAX_ = 0x7fffffff
 } mfa_status_t;
 
 /* GEMMOperandPrecision (Sources/FlashAttention/GEMM/GEMMOperandPrecision.swift:22-27),
@@ -55,7 +60,9 @@ typedef enum mfa_precision {
   MFA_PRECISION_BF16 = 2,
   MFA_PRECISION_INT8 = 3,
   MFA_PRECISION_INT4 = 4,
-  MFA_PRECISION_UNSET = -1 /* Swift `nil` for inputMemoryPrecision (resolves to FP16) */
+  MFA_PRECISION_UNSET = -1, /* Swift `nil` for inputMemoryPrecision (resolves to FP16) */
+  MFA_PRECISION_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_PRECISION_RANGE_MAX_ = 0x7fffffff
 } mfa_precision_t;
 
 /* AttentionKernelType (Attention/AttentionKernelType.swift:10-29). */
@@ -63,7 +70,9 @@ typedef enum mfa_kernel_type {
   MFA_KERNEL_FORWARD = 0,
   MFA_KERNEL_BACKWARD_QUERY = 1,
   MFA_KERNEL_BACKWARD_KEY_VALUE = 2,
-  MFA_KERNEL_MLA_COMPRESSED = 3
+  MFA_KERNEL_MLA_COMPRESSED = 3,
+  MFA_KERNEL_TYPE_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_KERNEL_TYPE_RANGE_MAX_ = 0x7fffffff
 } mfa_kernel_type_t;
 
 /* AttentionOperand (Attention/AttentionOperand.swift:9-24); buffer slots of
@@ -83,7 +92,9 @@ typedef enum mfa_operand {
   MFA_OPERAND_dS = 11,
   MFA_OPERAND_dK = 12,
   MFA_OPERAND_dQ = 13,
-  MFA_OPERAND_COUNT = 14
+  MFA_OPERAND_COUNT = 14,
+  MFA_OPERAND_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_OPERAND_RANGE_MAX_ = 0x7fffffff
 } mfa_operand_t;
 
 /* Returns the reference buffer slot of an operand, or -1 (AttentionOperand.swift:50-67). */
@@ -95,14 +106,18 @@ typedef enum mfa_sparsity {
   MFA_SPARSITY_NONE = 0,
   MFA_SPARSITY_CAUSAL = 1,
   MFA_SPARSITY_SLIDING_WINDOW = 2,
-  MFA_SPARSITY_CUSTOM = 3
+  MFA_SPARSITY_CUSTOM = 3,
+  MFA_SPARSITY_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_SPARSITY_RANGE_MAX_ = 0x7fffffff
 } mfa_sparsity_t;
 
 /* SparseMaskDescriptor.MaskType (AttentionDescriptor.swift:47-51). */
 typedef enum mfa_mask_type {
   MFA_MASK_DENSE = 0,         /* mask buffer = fp32 additive [B, H, R, C] added to QK^T */
   MFA_MASK_SPARSE_RANGES = 1, /* mask buffer = uint32x2 [B, H_kv, R] half-open key ranges */
-  MFA_MASK_BLOCK_SPARSE = 2   /* flag only; ranges built by mfa_sparse_build_block_sparse */
+  MFA_MASK_BLOCK_SPARSE = 2, /* flag only; ranges built by mfa_sparse_build_block_sparse */
+  MFA_MASK_TYPE_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_MASK_TYPE_RANGE_MAX_ = 0x7fffffff
 } mfa_mask_type_t;
 
 /* AttentionDescriptor (AttentionDescriptor.swift:17-43). */
@@ -188,7 +203,9 @@ typedef enum mfa_broadcast_mode {
   MFA_BROADCAST_GROUPED_QUERY = 1,
   MFA_BROADCAST_MULTI_QUERY = 2,
   MFA_BROADCAST_CROSS_ATTENTION = 3,
-  MFA_BROADCAST_CUSTOM = 4
+  MFA_BROADCAST_CUSTOM = 4,
+  MFA_BROADCAST_MODE_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_BROADCAST_MODE_RANGE_MAX_ = 0x7fffffff
 } mfa_broadcast_mode_t;
 
 /* MultiHeadDispatchStrategy (MultiHeadAttentionDescriptor.swift:121-159). All strategies
@@ -198,7 +215,9 @@ typedef enum mfa_dispatch_strategy {
   MFA_DISPATCH_PER_BATCH_HEAD = 0,
   MFA_DISPATCH_PER_BATCH = 1,
   MFA_DISPATCH_BATCHED = 2,
-  MFA_DISPATCH_AUTO = 3
+  MFA_DISPATCH_AUTO = 3,
+  MFA_DISPATCH_STRATEGY_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_DISPATCH_STRATEGY_RANGE_MAX_ = 0x7fffffff
 } mfa_dispatch_strategy_t;
 
 /* MultiHeadAttentionDescriptor (MultiHeadAttentionDescriptor.swift:162-214). */
@@ -289,14 +308,18 @@ int mfa_last_launches(mfa_kernel_plan_t* out);
 typedef enum mfa_quantization_mode {
   MFA_QUANT_TENSOR_WISE = 0,
   MFA_QUANT_BLOCKWISE = 1,
-  MFA_QUANT_ROW_WISE = 2
+  MFA_QUANT_ROW_WISE = 2,
+  MFA_QUANTIZATION_MODE_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_QUANTIZATION_MODE_RANGE_MAX_ = 0x7fffffff
 } mfa_quantization_mode_t;
 
 /* QuantizationStrategy (GEMMQuantization.swift:45-55). */
 typedef enum mfa_quantization_strategy {
   MFA_QUANT_STRATEGY_LEGACY = 0,
   MFA_QUANT_STRATEGY_ASYMMETRIC = 1,
-  MFA_QUANT_STRATEGY_SYMMETRIC = 2
+  MFA_QUANT_STRATEGY_SYMMETRIC = 2,
+  MFA_QUANTIZATION_STRATEGY_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_QUANTIZATION_STRATEGY_RANGE_MAX_ = 0x7fffffff
 } mfa_quantization_strategy_t;
 
 /* A QuantizedTensor (GEMMQuantization.swift:681-700) as the kernels consume it.
@@ -410,7 +433,9 @@ typedef enum mfa_quantized_slot_key {
   MFA_QSLOT_K_STRIDES, MFA_QSLOT_V_STRIDES, MFA_QSLOT_O_STRIDES, MFA_QSLOT_MASK_BUFFER,
   MFA_QSLOT_MASK_METADATA, MFA_QSLOT_NUM_HEADS, MFA_QSLOT_NUM_KEY_VALUE_HEADS,
   MFA_QSLOT_HEAD_DIMENSION, MFA_QSLOT_SEQUENCE_LENGTH, MFA_QSLOT_SCRATCH0, MFA_QSLOT_SCRATCH1,
-  MFA_QSLOT_COUNT
+  MFA_QSLOT_COUNT,
+  MFA_QUANTIZED_SLOT_KEY_RANGE_MIN_ = -0x7fffffff - 1, /* range sentinel (see mfa_status) */
+  MFA_QUANTIZED_SLOT_KEY_RANGE_MAX_ = 0x7fffffff
 } mfa_quantized_slot_key_t;
 
 /* Layout.index(key) of QuantizedKernelLayoutManifest.layout(for: kernel): the slot, or -1

@@ -14,9 +14,14 @@ import numpy as np
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(_REPO, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "libmfa_oracle.so")
+# MFA_ORACLE_LIB: another build of the same source, e.g. the sanitizer build
+# (oracle/_asan/libmfa_oracle.so, tools/asan_check.sh).
+_ALT = os.environ.get("MFA_ORACLE_LIB")
 
 
 def _load():
+    if _ALT:
+        return ctypes.CDLL(_ALT)
     src = os.path.join(ORACLE_DIR, "mfa_oracle.c")
     if not os.path.exists(ORACLE_LIB) or os.path.getmtime(ORACLE_LIB) < os.path.getmtime(src):
         subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
