@@ -792,7 +792,10 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     if (has_next) ld_load(hn, tn);
     // MSK at D = 256 spills a few registers; their reloads wait for every outstanding load
     // (vmcnt(0)), so the next step's tiles are issued after the S/dP chains, where none is left.
-    constexpr bool late_dma = MSK && DP >= 256;
+#ifndef MFA_BWD_LATE_ALL
+#define MFA_BWD_LATE_ALL 0  // diagnostic builds: the unmasked D = 256 key phase issues late too
+#endif
+    constexpr bool late_dma = (MSK || MFA_BWD_LATE_ALL) && DP >= 256;
     auto issue_next = [&]() {
       if (MSK && has_next) am_issue(hn, tn, am0 + (cur ^ 1) * BQ * BK);
       if (!(spread_dma<DP>() && !MSK) && has_next) {

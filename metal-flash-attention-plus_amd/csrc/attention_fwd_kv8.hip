@@ -28,7 +28,14 @@
 
 namespace mfa {
 
-template <class E, int DP, int BK, int SRC>
+// BW (round 6): block-wise K/V scales (and zero points) applied on load, at D <= 128 with the
+// block size a multiple of the chunk width and untransposed K/V: a thread's chunk lies in one
+// scale block, so its widening takes one scale and one zero point, loaded with the chunk's bytes
+// a tile ahead, and writes (q - zp) * s rounded to E — the values the dequantisation pass
+// writes (kv_dequant.hip), so the MFMA operands, O and L are bit-identical to that path
+// (AttentionKernel+OuterProduct.swift:301-316 and AttentionKernel+Accumulate.swift:461-476
+// apply the block scales inside the reference kernel the same way).
+template <class E, int DP, int BK, int SRC, bool BW = false>
 __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   constexpr int NT = 512, BQ = 128, ND = DP / 32;
   constexpr int TILEB = BK * DP * 2;
@@ -46,6 +53,7 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   // each lane's own chunk (one 16-byte piece, or two 4-byte pieces for INT4), read back by the
   // same lane just before its widening — a counted vmcnt wait, no barrier.
   constexpr bool RAWLDS = DP == 256;
+  static_assert(!(BW && RAWLDS), "block-wise scales on load: D <= 128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -85,6 +93,9 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   const int vbytes = (int)((int64_t)(p.C - 1) * vss + (p.D >> SH));
   const int kro = cvalid ? cr * kss + (geo.col >> SH) : 0x40000000;
   const int vro = cvalid ? cr * vss + (geo.col >> SH) : 0x40000000;
+  // rk / rv: the bytes of the next tile to widen.  Each is reloaded (tile s + 2) as soon as
+  // its widening into tile s + 1's slot has been issued, one step ahead of its use.
+  uint4 rk = make_uint4(0u, 0u, 0u, 0u), rv = rk;
   // This thread's chunk of tile t's K (V) bytes.
   auto load1 = [&](const char* head, int ss, int bytes, int ro, int t) -> uint4 {
     const int tb = t * ss;
@@ -102,6 +113,35 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   };
   auto loadk = [&](int t) { return load1(khead, kss, kbytes, kro, t); };
   auto loadv = [&](int t) { return load1(vhead, vss, vbytes, vro, t); };
+  // BW: the scale-block row of this thread's chunk for the next load (loads run in tile order),
+  // and the pending chunk's scale, zero point and validity.
+  BlockRow kbr, vbr;
+  int kcb = 0, vcb = 0;
+  float ksc = 0.f, kzb = 0.f, vsc = 0.f, vzb = 0.f;
+  bool kok = false, vok = false;
+  if constexpr (BW) {
+    kbr.init(quant_row(p.k, b, kvh) + cr + kbeg, p.k.bsize);
+    vbr.init(quant_row(p.v, b, kvh) + cr + kbeg, p.v.bsize);
+    kcb = geo.col / p.k.bsize;
+    vcb = geo.col / p.v.bsize;
+  }
+  auto scale_of = [&](const Operand& op, BlockRow& br, int cb, int t, float& sc, float& z,
+                      bool& ok) {
+    ok = cvalid && t + cr < p.C;
+    const int i = br.q * op.bcols + cb;
+    sc = ok ? op.bscale[i] : 0.f;
+    z = ok && op.bzp ? (float)op.bzp[i] : 0.f;
+    br.advance(BK, op.bsize);
+  };
+  // The next tile's chunk bytes (and BW: its scale) into the staging registers.
+  auto nextk = [&](int t) {
+    rk = loadk(t);
+    if constexpr (BW) scale_of(p.k, kbr, kcb, t, ksc, kzb, kok);
+  };
+  auto nextv = [&](int t) {
+    rv = loadv(t);
+    if constexpr (BW) scale_of(p.v, vbr, vcb, t, vsc, vzb, vok);
+  };
   // LDS byte ring (RAWLDS): K slots 0, 1, then V slots 0, 1, of 512 chunks each.
   constexpr int NPC = CB == 16 ? 1 : CB / 4;  // DMA instructions per operand per tile
   constexpr int RSLOT = NT * CB;
@@ -133,9 +173,22 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   };
   auto dmak = [&](int t, int sl) { raw_dma(khead, kss, kbytes, kro, t, rawb + sl * RSLOT); };
   auto dmav = [&](int t, int sl) { raw_dma(vhead, vss, vbytes, vro, t, rawb + (2 + sl) * RSLOT); };
-  auto widen = [&](char* img, const uint4& raw, float zp, auto half_c) {
+  // The staged K (V) chunk's half HF widened into image img.
+  auto widen_k = [&](char* img, auto half_c) {
     constexpr int HF = decltype(half_c)::value;
-    widen_store<E, DP, SRC, HF>(img, cr, ch0 + HF, raw, zp);
+    if constexpr (BW)
+      *reinterpret_cast<uint4*>(img + TileA<DP>::off(cr, ch0 + HF)) =
+          widen_block<E, SRC, HF>(rk, ksc, kzb, kok);
+    else
+      widen_store<E, DP, SRC, HF>(img, cr, ch0 + HF, rk, zk);
+  };
+  auto widen_v = [&](char* img, auto half_c) {
+    constexpr int HF = decltype(half_c)::value;
+    if constexpr (BW)
+      *reinterpret_cast<uint4*>(img + TileA<DP>::off(cr, ch0 + HF)) =
+          widen_block<E, SRC, HF>(rv, vsc, vzb, vok);
+    else
+      widen_store<E, DP, SRC, HF>(img, cr, ch0 + HF, rv, zv);
   };
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
@@ -143,9 +196,6 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   const int q0 = (2 * pi + g) * BQ;
   const int qi = q0 + wg * 32 + l32;
   i16x8 qf[DP / 16];
-  // rk / rv: the bytes of the next tile to widen.  Each is reloaded (tile s + 2) as soon as
-  // its widening into tile s + 1's slot has been issued, one step ahead of its use.
-  uint4 rk, rv;
   if constexpr (RAWLDS) {
     dmak(kbeg, 0);
     dmav(kbeg, 0);
@@ -160,20 +210,20 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
       widen_half(sv, raw_read(rawb + 2 * RSLOT, hf), zv, hf);
     }
   } else {
-    rk = loadk(kbeg);
-    rv = loadv(kbeg);
+    nextk(kbeg);
+    nextv(kbeg);
     load_q2_raw<DP>(qf, p, b, h, qi, qi < p.R, hh);
   }
   prescale_q2<E, DP>(qf, c);
   if constexpr (!RAWLDS) {
-    widen(sk, rk, zk, H0());
-    widen(sv, rv, zv, H0());
+    widen_k(sk, H0());
+    widen_v(sv, H0());
     if constexpr (CE == 16) {
-      widen(sk, rk, zk, H1());
-      widen(sv, rv, zv, H1());
+      widen_k(sk, H1());
+      widen_v(sv, H1());
     }
-    rk = loadk(kbeg + BK);
-    rv = loadv(kbeg + BK);
+    nextk(kbeg + BK);
+    nextv(kbeg + BK);
   }
   __syncthreads();
 
@@ -206,10 +256,10 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
         }
       } else {
         if constexpr (CE == 16)
-          if (i == KP0) widen(knext, rk, zk, H0());
+          if (i == KP0) widen_k(knext, H0());
         if (i == KP1) {
-          widen(knext, rk, zk, std::integral_constant<int, CE == 16 ? 1 : 0>());
-          rk = loadk(t + 2 * BK);
+          widen_k(knext, std::integral_constant<int, CE == 16 ? 1 : 0>());
+          nextk(t + 2 * BK);
         }
       }
     };
@@ -227,10 +277,10 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
         }
       } else {
         if constexpr (CE == 16)
-          if (i == VP0) widen(vnext, rv, zv, H0());
+          if (i == VP0) widen_v(vnext, H0());
         if (i == VP1) {
-          widen(vnext, rv, zv, std::integral_constant<int, CE == 16 ? 1 : 0>());
-          rv = loadv(t + 2 * BK);
+          widen_v(vnext, std::integral_constant<int, CE == 16 ? 1 : 0>());
+          nextv(t + 2 * BK);
         }
       }
     };
@@ -290,6 +340,19 @@ size_t fwd_kv8_lds_bytes(int DP) {
 template <class E, int DP>
 static hipError_t launch_kv8(const FwdParams& q, int src, dim3 grid, hipStream_t stream) {
   constexpr int BK = kv8_bk<DP>();
+  if constexpr (DP <= 128) {
+    if (q.k.bscale) {
+      if (src == SRC_I8)
+        return launch(mfa_fwd2_kv8_kernel<E, DP, BK, SRC_I8, true>, grid, dim3(512), kv8_lds<DP>(),
+                      stream, q);
+      if (src == SRC_I4)
+        return launch(mfa_fwd2_kv8_kernel<E, DP, BK, SRC_I4, true>, grid, dim3(512), kv8_lds<DP>(),
+                      stream, q);
+      return hipErrorNotSupported;
+    }
+  } else {
+    if (q.k.bscale) return hipErrorNotSupported;
+  }
   if (src == SRC_I8)
     return launch(mfa_fwd2_kv8_kernel<E, DP, BK, SRC_I8>, grid, dim3(512), kv8_lds<DP>(), stream, q);
   if (src == SRC_I4)

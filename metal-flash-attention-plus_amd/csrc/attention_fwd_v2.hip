@@ -969,6 +969,19 @@ __global__ void __launch_bounds__(512, 2) mfa_fwd2_share_kv8_kernel(FwdParams p)
   fwd2_share_body<E, DP, BK, true, true, true, false, KVS>(p);
 }
 
+// Mirrored pairs: the light half of the pairs waits 8 x 512 cycles (~2 us) before its
+// prologue loads, so the heavy pairs (the critical path: ~7 us more loop than the lightest) get
+// the prologue's HBM burst first.  C2, one-process A/B over delays 0/4/8/12 and splits 4/8/12
+// (profiles/r06d_ab_prologue_delay.txt): 0.0733 -> 0.0721 ms at split 8 (+1.7 %), +0.4..0.7 %
+// in the other two runs.  A/B knobs: MFA_FWD_DELAY (rounds), MFA_FWD_DELAY_SPLIT (first
+// delayed pair index).
+static void set_prologue_delay(FwdParams& q, int npairs) {
+  const char* dl = mfa::dev_env("MFA_FWD_DELAY");
+  const char* ds = mfa::dev_env("MFA_FWD_DELAY_SPLIT");
+  q.pro_delay = dl ? atoi(dl) : 8;
+  q.pro_split = ds ? atoi(ds) : npairs / 2;
+}
+
 template <class E, int DP, int BK, bool MIRROR = true>
 static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
   // Adjacent pairs use ring 0 only (every step is shared, no merge).
@@ -986,18 +999,7 @@ static hipError_t launch_fwd2_share(const FwdParams& p, hipStream_t stream) {
     const char* xh = mfa::dev_env("MFA_SHARE_XCD");  // A/B: 0 deals pairs round-robin over heads
     q.xcd_heads = !(xh && xh[0] == '0');
   }
-  {
-    // Mirrored pairs: the light half of the pairs waits 8 x 512 cycles (~2 us) before its
-    // prologue loads, so the heavy pairs (the critical path: ~7 us more loop than the lightest)
-    // get the prologue's HBM burst first.  C2, one-process A/B over delays 0/4/8/12 and splits
-    // 4/8/12 (profiles/r06d_ab_prologue_delay.txt): 0.0733 -> 0.0721 ms at split 8 (+1.7 %),
-    // +0.4..0.7 % in the other two runs.  A/B knobs: MFA_FWD_DELAY (rounds),
-    // MFA_FWD_DELAY_SPLIT (first delayed pair index).
-    const char* dl = mfa::dev_env("MFA_FWD_DELAY");
-    const char* ds = mfa::dev_env("MFA_FWD_DELAY_SPLIT");
-    q.pro_delay = dl ? atoi(dl) : 8;
-    q.pro_split = ds ? atoi(ds) : npairs / 2;
-  }
+  set_prologue_delay(q, npairs);
   // Mirrored pairs store the final O image non-temporally; MFA_SHARE_NT=0 keeps plain stores
   // (A/B).
   // Mirrored pairs: deferred V0 (+1.2 % at C2 in one-process A/B) and non-temporal O image
@@ -1061,12 +1063,15 @@ static hipError_t launch_fwd2_pair(const FwdParams& p, hipStream_t stream) {
 // (the caller then takes the dequantisation pass).
 hipError_t fwd_share_kv8_dispatch(const FwdParams& p, int elem, int DP, int src,
                                   hipStream_t stream) {
-  if (DP != 128 || !p.mask.causal || p.mask.window || p.mask.ranges || p.mask.amask)
+  // (Block-wise K/V scales: the adjacent-pair on-load kernel, attention_fwd_kv8.hip.)
+  if (DP != 128 || !p.mask.causal || p.mask.window || p.mask.ranges || p.mask.amask ||
+      p.k.bscale || p.v.bscale)
     return hipErrorNotSupported;
   FwdParams q = p;
   q.nblk = (p.R + 127) / 128;
   const int blocks = q.nblk * p.B * p.H;
   if (blocks > 768 && !(q.nblk >= 64 && blocks <= 1536)) return hipErrorNotSupported;
+  set_prologue_delay(q, (q.nblk + 1) / 2);
   constexpr int BK = 64;
   constexpr int RING = 8 * BK * DP_KV8 * 2 + 4 * 32 * DP_KV8 * 2;
   constexpr int MERGE = 4 * (DP_KV8 / 32) * 16 * 64 * 4 + 4 * 2 * 64 * 4;

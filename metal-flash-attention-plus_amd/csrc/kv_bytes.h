@@ -21,6 +21,79 @@ __device__ __forceinline__ void widen_store(char* img, int r, int ch, const uint
   *reinterpret_cast<uint4*>(img + TileA<DP>::off(r, ch)) = dequant_fast<E, SRC>(q, zp);
 }
 
+// Blockwise-scaled chunk (round 6): 8 quantised elements of one scale block -> the 16-bit
+// TileA chunk holding (q - zp) * s rounded to E, as the dequantisation pass writes it
+// (mfa_stage.h convert_qchunk / dequant: (float)(q - zp) exact, one FP32 multiply, one rounding
+// to FP16 / BF16), so the MFMA operands are bit-identical to the pass's.  An invalid chunk (rows
+// past the operand's end, columns past D) is zero, as the pass's zero-filled copy reads.
+//   FP16, |zp| <= 896: q - zp exact in FP16 by dequant_fast (|q - zp| <= 1024), then
+//     v_fma_mix_f32 (FP16 operand x FP32 scale + 0: the FP32-rounded product) and one packed
+//     conversion: about 2 VALU per element;
+//   otherwise (BF16, or a zero point past that): q - zp in FP32 (byte -> float, subtract), the
+//     FP32 multiply, the conversion: about 3.5 per element.
+template <class E, int SRC, int HALF>
+__device__ __forceinline__ uint4 widen_block(const uint4 raw, float s, float zp, bool valid) {
+  uint32_t o[4];
+  // (Both forms give the same bits, so the choice is made per wave: a branch, not a select.)
+  if (E::prec == P_FP16 && __all(fabsf(zp) <= 896.f)) {
+    uint4 q;
+    if constexpr (SRC == SRC_I8)
+      q = HALF ? make_uint4(raw.z, raw.w, 0u, 0u) : make_uint4(raw.x, raw.y, 0u, 0u);
+    else
+      q = make_uint4(HALF ? raw.y : raw.x, 0u, 0u, 0u);
+    const uint4 n = dequant_fast<F16, SRC>(q, zp);
+    const uint32_t nw[4] = {n.x, n.y, n.z, n.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f16x2 v = __builtin_bit_cast(f16x2, nw[k]);
+      o[k] = pack_f16x2(__builtin_fmaf((float)v[0], s, 0.f), __builtin_fmaf((float)v[1], s, 0.f));
+    }
+  } else {
+    const float m = (SRC == SRC_I8 ? 128.f : 8.f) + zp;
+    float f[8];
+    if constexpr (SRC == SRC_I8) {
+      const uint32_t u0 = (HALF ? raw.z : raw.x) ^ 0x80808080u;
+      const uint32_t u1 = (HALF ? raw.w : raw.y) ^ 0x80808080u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f[k] = (float)((u0 >> (8 * k)) & 0xffu) - m;
+        f[4 + k] = (float)((u1 >> (8 * k)) & 0xffu) - m;
+      }
+    } else {
+      const uint32_t w = HALF ? raw.y : raw.x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = (float)((w >> (4 * k)) & 15u) - m;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // (mul_rn: no contraction with the conversion into one rounding; see mfa_stage.h dequant.)
+      const float a = mul_rn(f[2 * k], s), b = mul_rn(f[2 * k + 1], s);
+      if constexpr (E::prec == P_FP16)
+        o[k] = pack_f16x2(a, b);  // round to nearest even, as convert_qchunk
+      else
+        o[k] = (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);  // v_cvt_pk_bf16_f32
+    }
+  }
+  return valid ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Scale-block row index of a chunk's row, advanced one key tile (bk rows) at a time: the row
+// block q = row / bs and the row's place r = row % bs in it, without a division per tile.
+struct BlockRow {
+  int q, r;
+  __device__ __forceinline__ void init(int64_t row, int bs) {
+    q = (int)(row / bs);
+    r = (int)(row - (int64_t)q * bs);
+  }
+  __device__ __forceinline__ void advance(int bk, int bs) {
+    r += bk;
+    while (r >= bs) {
+      r -= bs;
+      ++q;
+    }
+  }
+};
+
 // One LDS-DMA wave-instruction of 4 bytes per lane (buffer_load_dword ... lds): lane l's dword
 // from base + voff lands at dst + 4·l (range-checked against nrec bytes, zeros past it).
 __device__ __forceinline__ void lds_dma4(const void* base, int nrec, int voff, char* dst) {

@@ -742,7 +742,7 @@ bool decode_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp) 
 }
 
 // The on-load shared-tile forward (attention_fwd_kv8.hip): FP16 or BF16 Q (the compute type),
-// per-tensor INT8 or INT4 K/V (any zero point), D % 16 == 0 with D <= 256 (padded to 64, 128
+// per-tensor INT8 or INT4 K/V (any zero point) or block-wise K/V (below), D % 16 == 0 with D <= 256 (padded to 64, 128
 // or 256), no masks, dense rows with 16-byte aligned byte offsets.  Causal at D = 128 runs the
 // mirrored shared-tile kernel's on-load instantiation where that schedule applies
 // (attention_fwd_v2.hip fwd_share_kv8_dispatch; the pass elsewhere).  MFA_KV8=0 routes these
@@ -754,7 +754,16 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
   if (!((elem == 1 && qp == MFA_PRECISION_FP16) || (elem == 2 && qp == MFA_PRECISION_BF16)))
     return false;
   if (kp != vp || (kp != MFA_PRECISION_INT8 && kp != MFA_PRECISION_INT4)) return false;
-  if (p.k.bscale || p.v.bscale) return false;
+  // Block-wise scales (round 6): both K and V block-wise, untransposed, D <= 128, block sizes
+  // a multiple of a thread's chunk (16 elements; 8 at D = 64), so each chunk takes one scale.
+  if (!p.k.bscale != !p.v.bscale) return false;
+  if (p.k.bscale) {
+    if (const char* e = mfa::dev_env("MFA_KV8_BW")) {  // =0: block-wise K/V take the pass (A/B)
+      if (e[0] == '0') return false;
+    }
+    const int ce = DP == 64 ? 8 : 16;
+    if (DP > 128 || p.k.qtr || p.v.qtr || p.k.bsize % ce || p.v.bsize % ce) return false;
+  }
   if ((DP != 64 && DP != 128 && DP != 256) || p.D % 16 != 0 || !(p.c_log2 > 0.f)) return false;
   const int sh = kp == MFA_PRECISION_INT4 ? 1 : 0;  // element -> byte offsets
   if (p.mask.amask || p.mask.ranges) return false;

@@ -288,6 +288,16 @@ __device__ __forceinline__ float mul_rn(float a, float b) {
   return a * b;
 }
 
+// Two FP32 values rounded to FP16 (round to nearest even) and packed, a in the low half.  An
+// explicit instruction: hipcc otherwise turns some fptrunc(fmul) pairs into v_fma_mixlo_f16, one
+// rounding of the exact product instead of FP32 then FP16, and different code paths then
+// disagree at FP16 ties (the block-wise dequantisation pass vs the on-load widening).
+__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Keeps a rarely taken, wave-uniform branch (edge / diagonal tile masking) a branch: without
 // it the compiler if-converts the body into per-element selects that then run on every tile.
 #define MFA_KEEP_BRANCH() asm volatile("" ::: "memory")

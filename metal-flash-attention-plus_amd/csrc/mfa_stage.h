@@ -51,7 +51,10 @@ __device__ __forceinline__ float dequant(const Operand& op, int qv, int64_t hrow
     const int64_t vc = op.qtr ? row : col;
     const int64_t bi = (vr / op.bsize) * op.bcols + vc / op.bsize;
     const int zp = op.bzp ? op.bzp[bi] : 0;
-    return (float)(qv - zp) * op.bscale[bi];
+    // One FP32 rounding of the product, then (at the caller) one rounding to the 16-bit type:
+    // mul_rn keeps hipcc from contracting the multiply and the conversion into v_fma_mixlo_f16
+    // (a single rounding), so every path holds the same values (kv_bytes.h widen_block).
+    return mul_rn((float)(qv - zp), op.bscale[bi]);
   }
   return (float)(qv - op.zp);  // per-tensor scale folded by the host
 }
@@ -175,6 +178,7 @@ __device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& 
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
     uint32_t packed = 0u;
+    float xs[2] = {0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int j = 2 * jj + e;
@@ -187,8 +191,13 @@ __device__ __forceinline__ uint4 convert_qchunk(const uint4 raw, const Operand& 
       }
       float x = 0.f;
       if (valid && d0 + j < D) x = dequant(op, qv, hrow, row, d0 + j);
-      packed |= (uint32_t)E::from_f32(x) << (16 * e);
+      if constexpr (E::prec == P_FP16)
+        xs[e] = x;
+      else
+        packed |= (uint32_t)E::from_f32(x) << (16 * e);
     }
+    // (FP16: the explicit conversion of kv_bytes.h widen_block, so both hold the same bits.)
+    if constexpr (E::prec == P_FP16) packed = pack_f16x2(xs[0], xs[1]);
     w[jj] = packed;
   }
   return make_uint4(w[0], w[1], w[2], w[3]);

@@ -100,7 +100,7 @@ def test_quantized_plans():
     # Dequant-exact forward, FP16 Q + per-tensor INT8 K/V: one kernel widening the bytes as
     # it stages them (attention_fwd_kv8.hip), no pass.
     qx = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16)
-    assert [r["name"] for r in mfa.quantized_plan(qx)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1>"]
+    assert [r["name"] for r in mfa.quantized_plan(qx)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, false>"]
     # backwardQuery: one dequantisation pass per quantised operand (kv_dequant.hip), then the
     # tuned 16-bit kernel on the dense copies (K/V tiles stream through LDS) ...
     assert [r["name"] for r in mfa.quantized_plan(qx, K.backwardQuery)] == \
@@ -117,15 +117,15 @@ def test_quantized_plans():
         ["mfa_bwd_kv_fast_kernel<F16, 128, 64, 1, false>"]
     # INT4 K/V with an FP16 Q: the same on-load kernel (SRC_I4 = 2).
     q4h = mfa.quantized_descriptor(base, P.FP16, P.INT4, P.INT4, B=1, H=16)
-    assert [r["name"] for r in mfa.quantized_plan(q4h)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2>"]
+    assert [r["name"] for r in mfa.quantized_plan(q4h)] == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2, false>"]
     # BF16 Q at the same shape, and FP16 Q at D = 256 (BASELINE configs[4]'s width): the
     # same on-load kernel, no pass.
     bb = mfa.AttentionDescriptor.make(8192, 8192, 128, low_precision=True, precision=P.BF16)
     qb = mfa.quantized_descriptor(bb, P.BF16, P.INT8, P.INT8, B=1, H=16)
-    assert [r["name"] for r in mfa.quantized_plan(qb)] == ["mfa_fwd2_kv8_kernel<BF16, 128, 64, 1>"]
+    assert [r["name"] for r in mfa.quantized_plan(qb)] == ["mfa_fwd2_kv8_kernel<BF16, 128, 64, 1, false>"]
     b256 = mfa.AttentionDescriptor.make(4096, 4096, 256, low_precision=True, precision=P.FP16)
     q256 = mfa.quantized_descriptor(b256, P.FP16, P.INT8, P.INT8, B=2, H=32)
-    assert [r["name"] for r in mfa.quantized_plan(q256)] == ["mfa_fwd2_kv8_kernel<F16, 256, 32, 1>"]
+    assert [r["name"] for r in mfa.quantized_plan(q256)] == ["mfa_fwd2_kv8_kernel<F16, 256, 32, 1, false>"]
     # Causal INT8 at the C2 shape: the mirrored shared-tile kernel widening K/V on load.
     c2 = mfa.AttentionDescriptor.make(4096, 4096, 128, causal=True, low_precision=True,
                                       precision=P.FP16)
@@ -144,6 +144,33 @@ def test_quantized_plans():
     qd = mfa.quantized_descriptor(dec, P.FP16, P.INT8, P.INT8, B=1, H=4)
     names = [r["name"] for r in mfa.quantized_plan(qd)]
     assert names == ["mfa_fwd_decode16_kernel<F16, 128, 1>", "mfa_decode_merge_kernel"], names
+
+
+def test_blockwise_kv_on_load_plans():
+    # Block-wise K/V scales (round 6): the on-load forward's block-wise instantiation, no
+    # dequantisation pass, at D <= 128 when the block size is a multiple of a thread's chunk
+    # (16 elements; 8 at D = 64); other block sizes, D = 256 and transposed K/V keep the pass.
+    def bw(bs, prec=P.INT8):
+        t = mfa.QuantizedTensor(None, int(prec), 1.0, 0)
+        t.block_scales, t.block_size = 0x1000, bs
+        return t
+
+    def names(D, bs, prec=P.INT8, causal=False, qp=P.FP16):
+        base = mfa.AttentionDescriptor.make(8192, 8192, D, causal=causal, low_precision=True,
+                                            precision=qp)
+        q = mfa.quantized_descriptor(base, qp, prec, prec, B=1, H=16)
+        return [r["name"] for r in mfa.quantized_plan(q, K.forward, None, bw(bs, prec), bw(bs, prec))]
+
+    assert names(128, 64) == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, true>"]
+    assert names(128, 16, P.INT4) == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 2, true>"]
+    assert names(128, 128, qp=P.BF16) == ["mfa_fwd2_kv8_kernel<BF16, 128, 64, 1, true>"]
+    assert names(64, 8) == ["mfa_fwd2_kv8_kernel<F16, 64, 64, 1, true>"]
+    # Causal at D = 128: the adjacent-pair on-load kernel with the mask (the mirrored on-load
+    # kernel takes per-tensor scales only).
+    assert names(128, 32, causal=True) == ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, true>"]
+    for D, bs in ((128, 24), (128, 8), (256, 64)):
+        n = names(D, bs)
+        assert n[:2] == ["mfa_kv_dequant_kernel<F16, 1>"] * 2, (D, bs, n)
 
 
 def test_kv8_override_takes_the_dequant_pass(monkeypatch):

@@ -789,7 +789,7 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, qp, monkeypatch):
     E = "F16" if qp == P.FP16 else "BF16"
     names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
     if kv == P.INT8 or D % 32 == 0:
-        assert names == [f"mfa_fwd2_kv8_kernel<{E}, {DP}, {32 if DP == 256 else 64}, {src}>"], names
+        assert names == [f"mfa_fwd2_kv8_kernel<{E}, {DP}, {32 if DP == 256 else 64}, {src}, false>"], names
     else:  # INT4 rows of D / 2 bytes off 16-byte alignment: the dequantisation pass
         assert names[0] == f"mfa_kv_dequant_kernel<{E}, 2>", names
 
@@ -818,6 +818,96 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, qp, monkeypatch):
         assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
     else:
         assert maxerr(o1, o2) < 1e-5 and maxerr(l1, l2) < 2e-2
+
+
+# Block-wise INT8 / INT4 K/V scales (and zero points) on load (round 6): the on-load forward's
+# block-wise instantiation widens each thread's chunk to (q - zp)·s rounded to the compute type,
+# one scale block per chunk (block size a multiple of 16; 8 at D = 64).  Held to the oracle on
+# the dequantised FP32 values and bit for bit to the dequantisation pass + 16-bit kernel path
+# (MFA_KV8_BW=0), whose dense copy holds the same values.  The block grid is over the
+# [B·H_kv·C, D] view (AttentionKernel+OuterProduct.swift:301-316, GEMMHeaders.swift:679-808);
+# ragged key counts put block rows across head boundaries.
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,bs,zp,qp,causal", [
+    (1, 4, 4, 512, 1000, 128, 64, False, P.FP16, False),
+    (1, 4, 2, 300, 333, 128, 16, True, P.FP16, False),    # GQA, zero points, partial tiles
+    (2, 2, 2, 256, 777, 96, 48, True, P.BF16, False),     # D 96 in 128-wide tiles, bs 48
+    (1, 8, 1, 256, 500, 128, 128, False, P.BF16, False),  # MQA
+    (1, 2, 2, 256, 300, 64, 8, True, P.FP16, False),      # D 64: 8-element chunks
+    (1, 4, 4, 640, 640, 128, 32, True, P.FP16, True),     # causal: adjacent pairs with the mask
+])
+def test_kv8_blockwise_on_load(gpu, kv, B, H, Hkv, R, C, D, bs, zp, qp, causal, monkeypatch):
+    rng = np.random.default_rng(R + C + D + bs)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    lim = 120 if kv == P.INT8 else 8
+    kq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    vq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    rows = B * Hkv * C
+    nb = ((rows + bs - 1) // bs) * ((D + bs - 1) // bs)
+    bcols = (D + bs - 1) // bs
+
+    def blocks(lo, hi):
+        s = rng.uniform(lo, hi, nb).astype(np.float32)
+        z = rng.integers(-3, 4, nb).astype(np.int32) if zp else np.zeros(nb, np.int32)
+        return s, z
+
+    (kscale, kzp), (vscale, vzp) = blocks(0.005, 0.03), blocks(0.005, 0.03)
+    r_idx = np.arange(rows)[:, None] // bs
+    c_idx = np.arange(D)[None, :] // bs
+    bi = (r_idx * bcols + c_idx)
+
+    def deq(q, sc, z):
+        x = q.reshape(rows, D).astype(np.float32)
+        return ((x - z[bi].astype(np.float32)) * sc[bi]).astype(np.float32).reshape(B, Hkv, C, D)
+
+    kd, vd = deq(kq, kscale, kzp), deq(vq, vscale, vzp)
+    base = mfa.AttentionDescriptor.make(R, C, D, causal=causal, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, qp), qp)
+    if kv == P.INT8:
+        kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
+    else:
+        pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
+        kt, vt = tdev(pack(kq.astype(np.int32)), torch.uint8), tdev(pack(vq.astype(np.int32)), torch.uint8)
+    keep = [tdev(kscale), tdev(vscale), torch.from_numpy(kzp).to(DEV), torch.from_numpy(vzp).to(DEV)]
+    tk = mfa.QuantizedTensor(kt.data_ptr(), int(kv), 1.0, 0)
+    tk.block_scales, tk.block_size = keep[0].data_ptr(), bs
+    tv = mfa.QuantizedTensor(vt.data_ptr(), int(kv), 1.0, 0)
+    tv.block_scales, tv.block_size = keep[1].data_ptr(), bs
+    if zp:
+        tk.block_zero_points, tv.block_zero_points = keep[2].data_ptr(), keep[3].data_ptr()
+    src = 1 if kv == P.INT8 else 2
+    DP = 64 if D <= 64 else 128
+    E = "F16" if qp == P.FP16 else "BF16"
+    names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    assert names == [f"mfa_fwd2_kv8_kernel<{E}, {DP}, 64, {src}, true>"], names
+
+    def run():
+        o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
+        l = torch.full((B, H, R), float("nan"), dtype=torch.float16, device=DEV)
+        mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+        torch.cuda.synchronize()
+        return o.cpu().numpy(), l.float().cpu().numpy()
+
+    o1, l1 = run()
+    monkeypatch.setenv("MFA_KV8_BW", "0")
+    n2 = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    assert n2[:2] == [f"mfa_kv_dequant_kernel<{E}, {src}>"] * 2, n2
+    o2, l2 = run()
+    monkeypatch.delenv("MFA_KV8_BW")
+    assert np.isfinite(o1).all()
+    Qs = seen(Q, qp)
+    # (BF16 holds (q - zp)·s to 8 significant bits: the pass path shows the same error.)
+    tol = 2e-3 if qp == P.FP16 else 2e-2
+    for h in sorted({0, H - 1}):
+        ref = ol.attention(Qs[:, h:h + 1], kd[:, h % Hkv:h % Hkv + 1], vd[:, h % Hkv:h % Hkv + 1],
+                           causal=causal)
+        assert maxerr(o1[:, h:h + 1], ref["O"]) < tol * max(1.0, np.abs(ref["O"]).max()), h
+        assert maxerr(l1[:, h:h + 1], ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max(), h
+    if not causal:  # (the pass path runs the mirrored kernel on causal shapes: another order)
+        assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
+    else:
+        assert maxerr(o1, o2) < 1e-3 * max(1.0, np.abs(o2).max())
 
 
 # Causal, FP16 / BF16 Q with per-tensor INT8 / INT4 K/V where the 16-bit path runs the mirrored

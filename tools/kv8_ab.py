@@ -31,6 +31,13 @@ def main():
              ("C5c bf16", 2, 32, 4096, 256, P.BF16, True), ("B4c fp16", 4, 32, 4096, 128, P.FP16, True),
              ("S8kw fp16", 1, 16, 8192, 128, P.FP16, False, 1024),
              ("C5w bf16", 2, 32, 4096, 256, P.BF16, False, 512)]
+    # --bw BS: block-wise K/V scales of block size BS (round 6), on load vs the pass (MFA_KV8_BW).
+    bw = 0
+    if "--bw" in sys.argv:
+        i = sys.argv.index("--bw")
+        bw = int(sys.argv[i + 1])
+        del sys.argv[i:i + 2]
+    knob = "MFA_KV8_BW" if bw else "MFA_KV8"
     if len(sys.argv) > 1:
         cases = [c for c in cases if any(c[0].startswith(x) for x in sys.argv[1].split(","))]
     for kv in (P.INT8, P.INT4):
@@ -49,6 +56,11 @@ def main():
             tq = mfa.quantized_tensor(q, qp)
             tk = mfa.quantized_tensor(k, kv, scale=0.01)
             tv = mfa.quantized_tensor(v, kv, scale=0.01)
+            if bw:
+                nbl = ((B * H * S + bw - 1) // bw) * ((D + bw - 1) // bw)
+                scs = [torch.rand(nbl, generator=g, device=dev) * 0.01 + 0.005 for _ in range(2)]
+                for t, sc in ((tk, scs[0]), (tv, scs[1])):
+                    t.block_scales, t.block_size = sc.data_ptr(), bw
             qa = mfa.QuantizedAttention()
             r = np.arange(S)
             lo = np.maximum(0, r - win) if win is not None else np.zeros(S, dtype=np.int64)
@@ -57,9 +69,9 @@ def main():
 
             def run(onload):
                 if onload:
-                    os.environ.pop("MFA_KV8", None)
+                    os.environ.pop(knob, None)
                 else:
-                    os.environ["MFA_KV8"] = "0"
+                    os.environ[knob] = "0"
                 qa.forward(desc, tq, tk, tv, o, l, stream=st)
 
             res = {True: [], False: []}
@@ -69,9 +81,9 @@ def main():
                     for _ in range(3):
                         run(onload)
                     if onload:
-                        os.environ.pop("MFA_KV8", None)
+                        os.environ.pop(knob, None)
                     else:
-                        os.environ["MFA_KV8"] = "0"
+                        os.environ[knob] = "0"
                     plans[onload] = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward,
                                                                            tq, tk, tv)]
                 torch.cuda.synchronize()
@@ -87,7 +99,7 @@ def main():
                         e1.record(st)
                         torch.cuda.synchronize()
                         res[onload].append(e0.elapsed_time(e1) / n)
-            os.environ.pop("MFA_KV8", None)
+            os.environ.pop(knob, None)
             a, b = min(res[True]), min(res[False])
             print(f"{'INT8' if kv == P.INT8 else 'INT4'} {name:9s} on-load {a * 1e3:8.1f} us "
                   f"({fl / a / 1e9:7.1f} TF)  pass {b * 1e3:8.1f} us ({fl / b / 1e9:7.1f} TF)  "
