@@ -758,9 +758,14 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
   // a multiple of a thread's chunk (16 elements; 8 at D = 64), so each chunk takes one scale.
   if (!p.k.bscale != !p.v.bscale) return false;
   if (p.k.bscale) {
-    if (const char* e = mfa::dev_env("MFA_KV8_BW")) {  // =0: block-wise K/V take the pass (A/B)
-      if (e[0] == '0') return false;
-    }
+    // The pass + tuned 16-bit kernel is faster where it runs (>= 128 query rows per kv head):
+    // the on-load widening of (q - zp)·s costs 0.83-0.94x of it at C3, D = 64 and causal C2
+    // (profiles/r06f_ab_kv8_blockwise.txt).  Below that the pass does not pay and the on-load
+    // kernel replaces the generic dequantise-on-store kernel.  MFA_KV8_BW=1 takes the on-load
+    // kernel at any size (no 16-bit scratch copy), =0 never (A/B).
+    const char* e = mfa::dev_env("MFA_KV8_BW");
+    if (e && e[0] == '0') return false;
+    if (!(e && e[0] == '1') && (int64_t)p.R * (p.H / p.Hkv) >= 128) return false;
     const int ce = DP == 64 ? 8 : 16;
     if (DP > 128 || p.k.qtr || p.v.qtr || p.k.bsize % ce || p.v.bsize % ce) return false;
   }

@@ -146,10 +146,27 @@ def test_quantized_plans():
     assert names == ["mfa_fwd_decode16_kernel<F16, 128, 1>", "mfa_decode_merge_kernel"], names
 
 
-def test_blockwise_kv_on_load_plans():
+def test_blockwise_kv_on_load_plans(monkeypatch):
     # Block-wise K/V scales (round 6): the on-load forward's block-wise instantiation, no
     # dequantisation pass, at D <= 128 when the block size is a multiple of a thread's chunk
     # (16 elements; 8 at D = 64); other block sizes, D = 256 and transposed K/V keep the pass.
+    # By default it runs where the pass does not (fewer than 128 query rows per kv head; the
+    # pass + 16-bit kernel is faster above); MFA_KV8_BW=1 takes it at any size.
+    base = mfa.AttentionDescriptor.make(8, 8192, 128, low_precision=True, precision=P.FP16)
+    few = mfa.quantized_descriptor(base, P.FP16, P.INT8, P.INT8, B=1, H=16, Hkv=4)
+
+    def bwt(bs):
+        t = mfa.QuantizedTensor(None, int(P.INT8), 1.0, 0)
+        t.block_scales, t.block_size = 0x1000, bs
+        return t
+    assert [r["name"] for r in mfa.quantized_plan(few, K.forward, None, bwt(64), bwt(64))] == \
+        ["mfa_fwd2_kv8_kernel<F16, 128, 64, 1, true>"]
+    big = mfa.quantized_descriptor(mfa.AttentionDescriptor.make(
+        8192, 8192, 128, low_precision=True, precision=P.FP16), P.FP16, P.INT8, P.INT8, B=1, H=16)
+    assert [r["name"] for r in mfa.quantized_plan(big, K.forward, None, bwt(64), bwt(64))][:2] == \
+        ["mfa_kv_dequant_kernel<F16, 1>"] * 2
+    monkeypatch.setenv("MFA_KV8_BW", "1")
+
     def bw(bs, prec=P.INT8):
         t = mfa.QuantizedTensor(None, int(prec), 1.0, 0)
         t.block_scales, t.block_size = 0x1000, bs

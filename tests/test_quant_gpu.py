@@ -837,6 +837,9 @@ def test_kv8_on_load(gpu, kv, B, H, Hkv, R, C, D, zps, qp, monkeypatch):
     (1, 4, 4, 640, 640, 128, 32, True, P.FP16, True),     # causal: adjacent pairs with the mask
 ])
 def test_kv8_blockwise_on_load(gpu, kv, B, H, Hkv, R, C, D, bs, zp, qp, causal, monkeypatch):
+    # (These shapes have >= 128 query rows per kv head, where the pass is the default: the
+    # on-load kernel is forced, MFA_KV8_BW=1, and held to the pass, MFA_KV8_BW=0.)
+    monkeypatch.setenv("MFA_KV8_BW", "1")
     rng = np.random.default_rng(R + C + D + bs)
     Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
     lim = 120 if kv == P.INT8 else 8
@@ -895,6 +898,8 @@ def test_kv8_blockwise_on_load(gpu, kv, B, H, Hkv, R, C, D, bs, zp, qp, causal, 
     assert n2[:2] == [f"mfa_kv_dequant_kernel<{E}, {src}>"] * 2, n2
     o2, l2 = run()
     monkeypatch.delenv("MFA_KV8_BW")
+    # The default route at these sizes is the pass.
+    assert [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)] == n2
     assert np.isfinite(o1).all()
     Qs = seen(Q, qp)
     # (BF16 holds (q - zp)·s to 8 significant bits: the pass path shows the same error.)
@@ -908,6 +913,69 @@ def test_kv8_blockwise_on_load(gpu, kv, B, H, Hkv, R, C, D, bs, zp, qp, causal, 
         assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
     else:
         assert maxerr(o1, o2) < 1e-3 * max(1.0, np.abs(o2).max())
+
+
+@pytest.mark.parametrize("kv", [P.INT8, P.INT4])
+@pytest.mark.parametrize("B,H,Hkv,R,C,D,bs,qp", [
+    (1, 8, 2, 16, 900, 128, 32, P.FP16),   # 64 query rows per kv head: on load by default
+    (2, 4, 4, 100, 333, 64, 16, P.BF16),   # 100 rows, D 64
+])
+def test_kv8_blockwise_few_rows_default(gpu, kv, B, H, Hkv, R, C, D, bs, qp, monkeypatch):
+    """Block-wise K/V with fewer than 128 query rows per kv head: the on-load kernel is the
+    default route (the pass does not pay there); held to the oracle and to the generic
+    dequantise-on-store kernel it replaces (MFA_KV8_BW=0)."""
+    rng = np.random.default_rng(R * 7 + C + bs)
+    Q = rng.standard_normal((B, H, R, D)).astype(np.float32)
+    lim = 120 if kv == P.INT8 else 8
+    kq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    vq = rng.integers(-lim, lim, (B, Hkv, C, D)).astype(np.int8)
+    rows, bcols = B * Hkv * C, (D + bs - 1) // bs
+    nb = ((rows + bs - 1) // bs) * bcols
+    ks, vs = (rng.uniform(0.005, 0.03, nb).astype(np.float32) for _ in range(2))
+    kz, vz = (rng.integers(-2, 3, nb).astype(np.int32) for _ in range(2))
+    bi = (np.arange(rows)[:, None] // bs) * bcols + np.arange(D)[None, :] // bs
+    deq = lambda q, sc, z: ((q.reshape(rows, D).astype(np.float32) - z[bi].astype(np.float32)) *
+                            sc[bi]).astype(np.float32).reshape(B, Hkv, C, D)
+    kd, vd = deq(kq, ks, kz), deq(vq, vs, vz)
+    base = mfa.AttentionDescriptor.make(R, C, D, low_precision=True, precision=qp)
+    desc = mfa.quantized_descriptor(base, qp, kv, kv, B=B, H=H, Hkv=Hkv)
+    tq = mfa.quantized_tensor(to_device(Q, qp), qp)
+    if kv == P.INT8:
+        kt, vt = tdev(kq.view(np.uint8), torch.uint8), tdev(vq.view(np.uint8), torch.uint8)
+    else:
+        pack = lambda x: ((x[..., 0::2] + 8) | ((x[..., 1::2] + 8) << 4)).astype(np.uint8)
+        kt, vt = tdev(pack(kq.astype(np.int32)), torch.uint8), tdev(pack(vq.astype(np.int32)), torch.uint8)
+    keep = [tdev(ks), tdev(vs), torch.from_numpy(kz).to(DEV), torch.from_numpy(vz).to(DEV)]
+    tk = mfa.QuantizedTensor(kt.data_ptr(), int(kv), 1.0, 0)
+    tv = mfa.QuantizedTensor(vt.data_ptr(), int(kv), 1.0, 0)
+    tk.block_scales, tk.block_zero_points, tk.block_size = keep[0].data_ptr(), keep[2].data_ptr(), bs
+    tv.block_scales, tv.block_zero_points, tv.block_size = keep[1].data_ptr(), keep[3].data_ptr(), bs
+    src = 1 if kv == P.INT8 else 2
+    E = "F16" if qp == P.FP16 else "BF16"
+    DP = 64 if D <= 64 else 128
+    names = [r["name"] for r in mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)]
+    assert names == [f"mfa_fwd2_kv8_kernel<{E}, {DP}, 64, {src}, true>"], names
+
+    def run():
+        o = torch.full((B, H, R, D), float("nan"), dtype=torch.float32, device=DEV)
+        l = torch.full((B, H, R), float("nan"), dtype=torch.float16, device=DEV)
+        mfa.QuantizedAttention().forward(desc, tq, tk, tv, o, l)
+        torch.cuda.synchronize()
+        return o.cpu().numpy(), l.float().cpu().numpy()
+
+    o1, l1 = run()
+    monkeypatch.setenv("MFA_KV8_BW", "0")
+    assert not mfa.quantized_plan(desc, mfa.KernelType.forward, tq, tk, tv)[-1]["name"].startswith(
+        "mfa_fwd2_kv8_kernel")
+    o2, _ = run()
+    monkeypatch.delenv("MFA_KV8_BW")
+    tol = 2e-3 if qp == P.FP16 else 2e-2
+    Qs = seen(Q, qp)
+    for h in sorted({0, H - 1}):
+        ref = ol.attention(Qs[:, h:h + 1], kd[:, h % Hkv:h % Hkv + 1], vd[:, h % Hkv:h % Hkv + 1])
+        assert maxerr(o1[:, h:h + 1], ref["O"]) < tol * max(1.0, np.abs(ref["O"]).max()), h
+        assert maxerr(l1[:, h:h + 1], ref["L"]) < 7e-3 + 2 ** -11 * np.abs(ref["L"]).max(), h
+    assert maxerr(o1, o2) < tol * max(1.0, np.abs(o2).max())
 
 
 # Causal, FP16 / BF16 Q with per-tensor INT8 / INT4 K/V where the 16-bit path runs the mirrored

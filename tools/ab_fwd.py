@@ -27,7 +27,7 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(7)
     causal = a.cfg == "C2"
-    B, H, S, D = (1, 16, 4096, 128) if a.cfg == "C2" else (1, 16, 8192, 128)
+    B, H, S, D = (1, 16, 4096, 128) if a.cfg in ("C2", "C2Q8") else (1, 16, 8192, 128)
     if a.cfg == "C2D64":
         B, H, S, D = 1, 32, 4096, 64
         causal = True
@@ -50,6 +50,19 @@ def main():
     q, k, v = (((torch.rand((B, H, S, D), generator=g, device=dev) * 2 - 1) * 0.25).to(dt)
                for _ in range(3))
     i8 = a.cfg == "C3I8"
+    q8c = a.cfg == "C2Q8"  # QuantizedAttention, per-tensor INT8 K/V, dequant-exact, causal C2
+    if q8c:
+        causal = True
+        kq, ks, _, _ = mfa.quantize(k.float().view(-1), mfa.Precision.INT8)
+        vq, vs, _, _ = mfa.quantize(v.float().view(-1), mfa.Precision.INT8)
+        torch.cuda.synchronize()
+        qdesc = mfa.quantized_descriptor(
+            mfa.AttentionDescriptor.make(S, S, D, causal=True, low_precision=True,
+                                         precision=mfa.Precision.FP16),
+            mfa.Precision.FP16, mfa.Precision.INT8, mfa.Precision.INT8, B=B, H=H)
+        tq = mfa.quantized_tensor(q, mfa.Precision.FP16)
+        tk = mfa.quantized_tensor(kq, mfa.Precision.INT8, scale=ks.item())
+        tv = mfa.quantized_tensor(vq, mfa.Precision.INT8, scale=vs.item())
     if i8:
         causal = False
         kq, ks, _, _ = mfa.quantize(k.float().view(-1), mfa.Precision.INT8)
@@ -68,7 +81,7 @@ def main():
         causal=causal)
     desc = mfa.MultiHeadDescriptor.make(base, B, H, S, D)
     mha = mfa.MultiHeadAttention()
-    if i8:
+    if i8 or q8c:
         qa = mfa.QuantizedAttention()
         run = lambda: qa.forward(qdesc, tq, tk, tv, o)
     else:
