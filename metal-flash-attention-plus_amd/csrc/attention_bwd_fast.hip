@@ -68,7 +68,16 @@ __device__ unsigned long long g_mfa_bstamps[1 << 18];
         g_mfa_bstamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + s_] = \
             bst_acc[s_];                                                           \
   } while (0)
+// Prologue points (cycles since the kernel's first stamp), in the second half of the buffer.
+#define BSTP(slot)                                                                        \
+  do {                                                                                    \
+    const unsigned long long tp_ = __builtin_amdgcn_s_memtime();                          \
+    if ((threadIdx.x & 63) == 0)                                                          \
+      g_mfa_bstamps[(1 << 17) + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + \
+                    (slot)] = tp_ - bst_t;                                                \
+  } while (0)
 #else
+#define BSTP(slot) do {} while (0)
 #define BST_DECL() do {} while (0)
 #define BST(slot) do {} while (0)
 #define BST_END() do {} while (0)
@@ -603,17 +612,14 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     const uint2* rrow = reinterpret_cast<const uint2*>(p.mask.ranges) + (int64_t)(b * p.Hkv + kvh) * p.R;
     const int ws = (int)min(p.mask.window_size, 0x7fffffffu);
     constexpr int PRE_N = 16;  // rows per thread whose loads are in flight together
-    // The first chunk runs on every thread (its loads guarded), so every lane issues load_kv.
-    int q0 = tid;
-    do {
-      uint2 rr[PRE_N];
-#pragma unroll
-      for (int j = 0; j < PRE_N; ++j) {
-        const int q = q0 + j * NT;
-        rr[j] = make_uint2(0u, 0x7fffffffu);
-        if (p.mask.ranges && q < p.R) rr[j] = rrow[q];
-      }
-      if (q0 == tid) load_kv();
+    // One chunk of PRE_N rows per thread.  D <= 128: the key block's K/V rows are loaded after
+    // the pre-pass, under the reduction, the step flags and the first tiles.  Issued between the
+    // range loads and their use (the previous form), they were waited for there: every load sits
+    // in an exec-masked branch, so hipcc cannot count them and the first use of a range waited
+    // with vmcnt(0) for the whole key block from HBM (13.3k of the prologue's 19.7k cycles per
+    // wave at band 8, tools/diag/bwd_stamps prologue points).  D = 256, at the register limit,
+    // keeps the previous form (moved, it spills).
+    auto pre_chunk = [&](const uint2 (&rr)[PRE_N], int q0) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < PRE_N; ++j) {
         const int q = q0 + j * NT;
@@ -629,8 +635,54 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
           if (pre) rgall[q] = lo >= hi ? make_int2(p.C, 0) : make_int2(lo, hi);
         }
       }
-      q0 += PRE_N * NT;
-    } while (q0 < p.R);
+    };
+    auto pre_load = [&](uint2 (&rr)[PRE_N], int q0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < PRE_N; ++j) {
+        const int q = q0 + j * NT;
+        rr[j] = make_uint2(0u, 0x7fffffffu);
+        if (p.mask.ranges && q < p.R) rr[j] = rrow[q];
+      }
+    };
+    if constexpr (DP <= 128) {
+      uint2 rr[PRE_N];
+      for (int q0 = tid; q0 < p.R; q0 += PRE_N * NT) {
+        pre_load(rr, q0);
+        if (q0 == tid) BSTP(5);
+        pre_chunk(rr, q0);
+        if (q0 == tid) BSTP(6);
+      }
+      load_kv();
+    } else {
+      int q0 = tid;
+      do {
+        uint2 rr[PRE_N];
+#pragma unroll
+        for (int j = 0; j < PRE_N; ++j) {
+          const int q = q0 + j * NT;
+          rr[j] = make_uint2(0u, 0x7fffffffu);
+          if (p.mask.ranges && q < p.R) rr[j] = rrow[q];
+        }
+        if (q0 == tid) load_kv();
+#pragma unroll
+        for (int j = 0; j < PRE_N; ++j) {
+          const int q = q0 + j * NT;
+          if (q < p.R) {
+            int lo = (int)min(rr[j].x, 0x7fffffffu);
+            int hi = (int)min(rr[j].y, (uint32_t)p.C);
+            if (p.mask.causal) hi = min(hi, q + 1);
+            if (p.mask.window) lo = max(lo, q - ws);
+            if (lo >= hi || (lo < k0 + BK && hi > k0)) {
+              rmin = min(rmin, q);
+              rmax = max(rmax, q);
+            }
+            if (pre) rgall[q] = lo >= hi ? make_int2(p.C, 0) : make_int2(lo, hi);
+          }
+        }
+        q0 += PRE_N * NT;
+      } while (q0 < p.R);
+    }
+    BSTP(0);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       rmin = min(rmin, __shfl_xor(rmin, o));
@@ -645,6 +697,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       rmax = max(rmax, red[w * 2 + 1]);
     }
     __syncthreads();
+    BSTP(1);
     qbeg = max(qbeg, (rmin / BQ) * BQ);
     qend = min(qend, rmax + 1);
     if (pre) {
@@ -662,6 +715,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
       }
     }
   }
+  BSTP(2);
   const int ntile = qbeg < qend ? (qend - qbeg + BQ - 1) / BQ : 0;
   const int ngroup = (p.H - kvh + p.Hkv - 1) / p.Hkv;  // query heads h = kvh + g*Hkv
   const int nsteps = ntile * ngroup;
@@ -770,7 +824,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_kv_fast_kernel(BwdParams p) {
     od.issue(ohead(kvh), qbeg, ob0);
     if (MSK) am_issue(kvh, qbeg, am0);
     ld_load(kvh, qbeg);
+    BSTP(3);
     wait_vm();
+    BSTP(4);
     ld_store(0, qbeg);
   }
   // Unconditionally drained before the loop: otherwise the K/V fragment loads count as

@@ -101,7 +101,7 @@ int main(int argc, char** argv) {
   const char* names[8] = {"L/D + DMA issue", "S(+dP) chain", "dP chain|P", "dV chain+dS", "dK chain", "wait_vm", "barrier+ld", "prologue"};
   double tot[8] = {0};
   int nw = 0;
-  for (size_t w = 0; w < (1 << 15); ++w) {
+  for (size_t w = 0; w < (1 << 14); ++w) {  // (the second half holds the prologue points)
     bool any = false;
     for (int s = 0; s < 8; ++s) any |= st8[w * 8 + s] != 0;
     if (!any) continue;
@@ -115,5 +115,18 @@ int main(int argc, char** argv) {
          band > 0 ? "in all" : "per step", all / nw);
   for (int s = 0; s < 8; ++s)
     printf("  %-14s %8.0f  (%.1f%%)\n", names[s], tot[s] / nw / (s == 7 ? 1 : nsteps), 100.0 * tot[s] / all);
+  // Prologue points, cycles from the wave's first stamp (medians over waves): 0 pre-pass loads
+  // and interval stores done, 1 row-range reduction done, 2 step flags done, 3 first tiles and
+  // L/D issued, 4 their wait done.
+  const char* pn[7] = {"pre-pass rows", "reduction", "step flags", "first tiles issued", "first tiles landed",
+                       "chunk 0 loads issued", "chunk 0 used"};
+  for (int k = 0; k < 7; ++k) {
+    std::vector<double> x;
+    for (size_t w = 0; w < (1 << 14); ++w)
+      if (st8[(1 << 17) + w * 8 + k]) x.push_back((double)st8[(1 << 17) + w * 8 + k]);
+    if (x.empty()) continue;
+    std::sort(x.begin(), x.end());
+    printf("  prologue point %-20s med %8.0f  p90 %8.0f cycles\n", pn[k], x[x.size() / 2], x[x.size() * 9 / 10]);
+  }
   return 0;
 }
