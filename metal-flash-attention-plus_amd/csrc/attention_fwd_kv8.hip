@@ -114,10 +114,14 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
   auto loadk = [&](int t) { return load1(khead, kss, kbytes, kro, t); };
   auto loadv = [&](int t) { return load1(vhead, vss, vbytes, vro, t); };
   // BW: the scale-block row of this thread's chunk for the next load (loads run in tile order),
-  // and the pending chunk's scale, zero point and validity.
+  // and the pending chunk's raw scale and zero-point bits and validity.  The scale loads are
+  // unconditional (an invalid chunk reads block 0; a missing zero-point table reads the scale
+  // table) and their values are used only at the next step's widening: a load under a branch,
+  // or used right away, made hipcc wait with vmcnt(0) after it, which also waited for the
+  // chunk's byte load issued just before (every step, in the first build).
   BlockRow kbr, vbr;
   int kcb = 0, vcb = 0;
-  float ksc = 0.f, kzb = 0.f, vsc = 0.f, vzb = 0.f;
+  uint32_t ksr = 0u, kzr = 0u, vsr = 0u, vzr = 0u;
   bool kok = false, vok = false;
   if constexpr (BW) {
     kbr.init(quant_row(p.k, b, kvh) + cr + kbeg, p.k.bsize);
@@ -125,22 +129,25 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
     kcb = geo.col / p.k.bsize;
     vcb = geo.col / p.v.bsize;
   }
-  auto scale_of = [&](const Operand& op, BlockRow& br, int cb, int t, float& sc, float& z,
+  auto scale_of = [&](const Operand& op, BlockRow& br, int cb, int t, uint32_t& sr, uint32_t& zr,
                       bool& ok) {
     ok = cvalid && t + cr < p.C;
-    const int i = br.q * op.bcols + cb;
-    sc = ok ? op.bscale[i] : 0.f;
-    z = ok && op.bzp ? (float)op.bzp[i] : 0.f;
+    const int i = ok ? br.q * op.bcols + cb : 0;
+    const uint32_t* sp = reinterpret_cast<const uint32_t*>(op.bscale);
+    const uint32_t* zq = op.bzp ? reinterpret_cast<const uint32_t*>(op.bzp) : sp;
+    sr = sp[i];
+    zr = zq[i];
     br.advance(BK, op.bsize);
   };
+  auto zp_of = [&](const Operand& op, uint32_t zr) { return op.bzp ? (float)(int)zr : 0.f; };
   // The next tile's chunk bytes (and BW: its scale) into the staging registers.
   auto nextk = [&](int t) {
     rk = loadk(t);
-    if constexpr (BW) scale_of(p.k, kbr, kcb, t, ksc, kzb, kok);
+    if constexpr (BW) scale_of(p.k, kbr, kcb, t, ksr, kzr, kok);
   };
   auto nextv = [&](int t) {
     rv = loadv(t);
-    if constexpr (BW) scale_of(p.v, vbr, vcb, t, vsc, vzb, vok);
+    if constexpr (BW) scale_of(p.v, vbr, vcb, t, vsr, vzr, vok);
   };
   // LDS byte ring (RAWLDS): K slots 0, 1, then V slots 0, 1, of 512 chunks each.
   constexpr int NPC = CB == 16 ? 1 : CB / 4;  // DMA instructions per operand per tile
@@ -178,7 +185,7 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
     constexpr int HF = decltype(half_c)::value;
     if constexpr (BW)
       *reinterpret_cast<uint4*>(img + TileA<DP>::off(cr, ch0 + HF)) =
-          widen_block<E, SRC, HF>(rk, ksc, kzb, kok);
+          widen_block<E, SRC, HF>(rk, __builtin_bit_cast(float, ksr), zp_of(p.k, kzr), kok);
     else
       widen_store<E, DP, SRC, HF>(img, cr, ch0 + HF, rk, zk);
   };
@@ -186,7 +193,7 @@ __global__ void __launch_bounds__(512, 1) mfa_fwd2_kv8_kernel(FwdParams p) {
     constexpr int HF = decltype(half_c)::value;
     if constexpr (BW)
       *reinterpret_cast<uint4*>(img + TileA<DP>::off(cr, ch0 + HF)) =
-          widen_block<E, SRC, HF>(rv, vsc, vzb, vok);
+          widen_block<E, SRC, HF>(rv, __builtin_bit_cast(float, vsr), zp_of(p.v, vzr), vok);
     else
       widen_store<E, DP, SRC, HF>(img, cr, ch0 + HF, rv, zv);
   };

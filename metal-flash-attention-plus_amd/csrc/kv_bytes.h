@@ -87,9 +87,15 @@ struct BlockRow {
   }
   __device__ __forceinline__ void advance(int bk, int bs) {
     r += bk;
-    while (r >= bs) {
-      r -= bs;
-      ++q;
+    if (bs >= bk) {  // at most one block boundary per tile: no loop
+      const bool w = r >= bs;
+      r -= w ? bs : 0;
+      q += w ? 1 : 0;
+    } else {
+      while (r >= bs) {
+        r -= bs;
+        ++q;
+      }
     }
   }
 };

@@ -760,7 +760,8 @@ bool kv8_eligible(const mfa::FwdParams& p, int elem, int qp, int kp, int vp, int
   if (p.k.bscale) {
     // The pass + tuned 16-bit kernel is faster where it runs (>= 128 query rows per kv head):
     // the on-load widening of (q - zp)·s costs 0.83-0.94x of it at C3, D = 64 and causal C2
-    // (profiles/r06f_ab_kv8_blockwise.txt).  Below that the pass does not pay and the on-load
+    // (profiles/r06j_ab_kv8_blockwise.txt; each element is widened once per
+    // pair of query blocks that reads it, 32 times at C3, where the pass widens it once).  Below that the pass does not pay and the on-load
     // kernel replaces the generic dequantise-on-store kernel.  MFA_KV8_BW=1 takes the on-load
     // kernel at any size (no 16-bit scratch copy), =0 never (A/B).
     const char* e = mfa::dev_env("MFA_KV8_BW");

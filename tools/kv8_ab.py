@@ -68,7 +68,9 @@ def main():
             fl = 4.0 * B * H * D * float(np.maximum(hi - lo + 1, 0).sum())
 
             def run(onload):
-                if onload:
+                if onload and bw:
+                    os.environ[knob] = "1"  # (block-wise: on load only when forced at these sizes)
+                elif onload:
                     os.environ.pop(knob, None)
                 else:
                     os.environ[knob] = "0"
@@ -80,7 +82,9 @@ def main():
                 for onload in (True, False):
                     for _ in range(3):
                         run(onload)
-                    if onload:
+                    if onload and bw:
+                        os.environ[knob] = "1"
+                    elif onload:
                         os.environ.pop(knob, None)
                     else:
                         os.environ[knob] = "0"
