@@ -48,6 +48,21 @@ constexpr bool kBwdKv256Interleave = true;
 template <int DP>
 constexpr bool spread_dma() { return DP >= MFA_SPREAD_MIN_DP; }
 
+// Diagnostic builds only: MFA_BWDQ_DMA_AT = 1 / 2 issues backwardQuery's next tile after the
+// S / dP chain instead of at the step's top.  Stamped, the later issue looked 20 % faster at
+// D = 256, but the stamps themselves had slowed that kernel by 46 %; the library A/B puts all
+// three placements within 0.5-1.4 % of each other.
+#ifndef MFA_BWDQ_DMA_AT
+#define MFA_BWDQ_DMA_AT 0
+#endif
+#define MFA_BWDQ_ISSUE_AT(at)                                                        \
+  do {                                                                               \
+    if (MFA_BWDQ_DMA_AT == (at) && !QKV && t + BT < kend) {                          \
+      kd.issue(khead, t + BT, kb0 + (cur ^ 1) * TILEB);                              \
+      vd.issue(vhead, t + BT, vb0 + (cur ^ 1) * TILEB);                              \
+    }                                                                                \
+  } while (0)
+
 // Diagnostic build only (tools/diag/bwd_stamps.hip defines MFA_BSTAMPS): per-wave shader-clock
 // totals of the backwardKeyValue phases, into a buffer no output is computed from.
 #ifdef MFA_BSTAMPS
@@ -197,6 +212,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
   char* const rawv = rawk + 2 * KB::SLOT;
 
   const int tid = threadIdx.x;
+  BST_DECL();  // (diagnostic builds: the backwardQuery phases, tools/diag/bwd_stamps q)
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int rbase[2] = {TileA<DP>::row_base(l32, hh, 0), TileA<DP>::row_base(l32, hh, 1)};
@@ -219,6 +235,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
                               (int64_t)h * p.dO_op.sh + (int64_t)qq * p.dO_op.ss,
                      qvalid, p.D, hh);
   }
+  BSTP(0);
 
   // K/V ring: issue the first tile before the D prologue so its latency hides behind it.
   int kend = p.C;
@@ -311,6 +328,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     }
   }
 
+  BSTP(1);
   // D = scale · Σ_d dO∘O (computeD, Softmax.swift:31-236): dO as stored (16-bit), O fp32.
   float dsum = 0.f;
   if (qvalid) {
@@ -328,6 +346,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     }
   }
   dsum = cross_half_sum(dsum);
+  BSTP(2);
   const float Drow = p.dscale * dsum;
   float Lrow = __builtin_inff();
   if (qvalid) {
@@ -357,7 +376,9 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) dq[dt] = zero16();
 
+  BSTP(3);
   wait_vm();
+  BSTP(4);
   if constexpr (QKV) {
     // The first tile's bytes are in (the second's may be too): widen the first.
     __asm__ __volatile__("" ::: "memory");
@@ -370,6 +391,8 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     }
   }
   __syncthreads();
+  BSTP(5);
+  BST(7);
   int cur = 0;
   for (int t = kbeg; t < kend; t += BT) {
     if constexpr (QKV) {
@@ -378,12 +401,13 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
         kq.dma(khead, kss, kbytes, t + 2 * BT, rawk + cur * KB::SLOT);
         vq.dma(vhead, vss, vbytes, t + 2 * BT, rawv + cur * KB::SLOT);
       }
-    } else if (t + BT < kend) {
+    } else if (MFA_BWDQ_DMA_AT == 0 && t + BT < kend) {
       kd.issue(khead, t + BT, kb0 + (cur ^ 1) * TILEB);
       vd.issue(vhead, t + BT, vb0 + (cur ^ 1) * TILEB);
     }
     const char* kt = kb0 + cur * TILEB;
     const char* vt = vb0 + cur * TILEB;
+    BST(0);
     // S^T = K·Q^T; masks; dP^T = V·dO^T with P^T = exp2(S^T·c − L) computed between its
     // MFMAs; dQ^T += K^T·dS^T with each k-step's dS^T = P^T∘(dP^T·scale − D) computed under
     // the previous k-step's MFMAs.
@@ -439,6 +463,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
     } else {
       rows_chain<A, NJ>(kt, qf, s, rbase, [](int) {});
     }
+    MFA_BWDQ_ISSUE_AT(1);
     if constexpr (MSK) {
       if (t >= tin_lo && min(t + BT, p.C) <= tin_hi) {
         if (p.mask.amask) {
@@ -467,6 +492,7 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
         mask_outside<NJ>(s, lo, hi, kMaskValue);
       }
     }
+    BST(1);
     {
       constexpr int EPM = 16 / DS;  // P elements per dP MFMA (NJ*16 over DS*NJ MFMAs)
       rows_chain<A, NJ>(vt, dof, dp, rbase, [&](int i) {
@@ -477,6 +503,8 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
         }
       });
     }
+    MFA_BWDQ_ISSUE_AT(2);
+    BST(2);
     {
       // dS^T of k-step jk = registers 8*(jk&1)..+7 of sub-tile jk>>1, packed as the B operand.
       i16x8 sb[NJ * 2];
@@ -502,8 +530,11 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
         }
       });
     }
+    BST(3);
     wait_vm();
+    BST(4);
     __syncthreads();
+    BST(5);
     cur ^= 1;
   }
 
@@ -521,6 +552,8 @@ __global__ void __launch_bounds__(256, 1) mfa_bwd_q_fast_kernel(BwdParams p) {
                           dq[dt][4 * g + 3] * mul);
       }
   }
+  BST(6);
+  BST_END();
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1,8 +1,9 @@
 // bwd_stamps.hip — diagnostic build of the fast backward with per-wave phase cycle totals of
 // backwardKeyValue (development tool; not part of libmfa_amd.so).  Build: make -C tools/diag
-// Run: tools/diag/bwd_stamps [B] [H] [S] [D] [band]   (fp16, non-causal; band > 0: sparse
-// ranges of `band` 128-key blocks per 128-row block, as bench.py's buildBlockSparse row, which
-// runs the mask instantiation)
+// Run: tools/diag/bwd_stamps [B] [H] [S] [D] [band] [phase]   (fp16, non-causal; band > 0:
+// sparse ranges of `band` 128-key blocks per 128-row block, as bench.py's buildBlockSparse row,
+// which runs the mask instantiation; phase 0 = backwardKeyValue (default), 1 = backwardQuery.
+// At most 16384 waves: B·H·S/32 for either phase)
 #define MFA_BSTAMPS 1
 #include "../../metal-flash-attention-plus_amd/csrc/attention_bwd_fast.hip"
 
@@ -39,6 +40,9 @@ int main(int argc, char** argv) {
   const int S = argc > 3 ? atoi(argv[3]) : 4096;
   const int D = argc > 4 ? atoi(argv[4]) : 128;
   const int band = argc > 5 ? atoi(argv[5]) : 0;
+  const int qphase = argc > 6 ? atoi(argv[6]) : 0;
+  const int kind = qphase ? 0 : 1;  // bwd_fast_dispatch: 0 = backwardQuery, 1 = backwardKeyValue
+  if ((size_t)B * H * S / 32 > (1u << 14)) { fprintf(stderr, "too many waves for the stamp buffer\n"); return 1; }
   const size_t n = (size_t)B * H * S * D;
   uint16_t *q, *k, *v, *dO;
   float *l, *dd, *o, *dq, *dk, *dv;
@@ -84,21 +88,24 @@ int main(int argc, char** argv) {
   CK(hipStreamCreate(&st));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 5; ++i) CK(mfa::bwd_fast_dispatch(p, 1, mfa::P_FP16, D, st));
+  for (int i = 0; i < 5; ++i) CK(mfa::bwd_fast_dispatch(p, kind, mfa::P_FP16, D, st));
   CK(hipEventRecord(e0, st));
-  for (int i = 0; i < 5; ++i) CK(mfa::bwd_fast_dispatch(p, 1, mfa::P_FP16, D, st));
+  for (int i = 0; i < 5; ++i) CK(mfa::bwd_fast_dispatch(p, kind, mfa::P_FP16, D, st));
   CK(hipEventRecord(e1, st));
   CK(hipStreamSynchronize(st));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= 5;
-  const double fl = 8.0 * D * (double)S * S * B * H;  // 4 GEMMs
-  printf("bwd_kv B=%d H=%d S=%d D=%d: %.3f ms, %.1f TFLOP/s executed\n", B, H, S, D, ms, fl / (ms * 1e-3) / 1e12);
+  const double fl = (qphase ? 6.0 : 8.0) * D * (double)S * S * B * H;  // 3 or 4 GEMMs
+  printf("%s B=%d H=%d S=%d D=%d band=%d: %.3f ms, %.1f TFLOP/s executed\n", qphase ? "bwd_q" : "bwd_kv", B, H, S,
+         D, band, ms, fl / (ms * 1e-3) / 1e12);
   std::vector<unsigned long long> st8(1 << 18);
   void* dsym;
   CK(hipGetSymbolAddress(&dsym, HIP_SYMBOL(mfa::g_mfa_bstamps)));
   CK(hipMemcpy(st8.data(), dsym, sizeof(unsigned long long) << 18, hipMemcpyDeviceToHost));
-  const char* names[8] = {"L/D + DMA issue", "S(+dP) chain", "dP chain|P", "dV chain+dS", "dK chain", "wait_vm", "barrier+ld", "prologue"};
+  const char* names_kv[8] = {"L/D + DMA issue", "S(+dP) chain", "dP chain|P", "dV chain+dS", "dK chain", "wait_vm", "barrier+ld", "prologue"};
+  const char* names_q[8] = {"DMA issue", "S chain+mask", "dP chain+P", "dQ chain+dS", "wait_vm", "barrier", "dQ store", "prologue"};
+  const char* const* names = qphase ? names_q : names_kv;
   double tot[8] = {0};
   int nw = 0;
   for (size_t w = 0; w < (1 << 14); ++w) {  // (the second half holds the prologue points)
@@ -110,16 +117,22 @@ int main(int argc, char** argv) {
   }
   double all = 0;
   for (int s = 0; s < 8; ++s) all += tot[s];
-  const int nsteps = band > 0 ? 1 : S / (D >= 256 ? 32 : 64);
+  const int nsteps = band > 0 ? 1 : S / (D >= 256 ? 32 : 64);  // (BT and BQ agree per D)
   printf("waves %d; per wave %s (shader cycles); per-wave total %.0f cycles:\n", nw,
          band > 0 ? "in all" : "per step", all / nw);
   for (int s = 0; s < 8; ++s)
-    printf("  %-14s %8.0f  (%.1f%%)\n", names[s], tot[s] / nw / (s == 7 ? 1 : nsteps), 100.0 * tot[s] / all);
+    printf("  %-14s %8.0f  (%.1f%%)\n", names[s], tot[s] / nw / (s == 7 || (qphase && s == 6) ? 1 : nsteps),
+           100.0 * tot[s] / all);
   // Prologue points, cycles from the wave's first stamp (medians over waves): 0 pre-pass loads
   // and interval stores done, 1 row-range reduction done, 2 step flags done, 3 first tiles and
   // L/D issued, 4 their wait done.
-  const char* pn[7] = {"pre-pass rows", "reduction", "step flags", "first tiles issued", "first tiles landed",
-                       "chunk 0 loads issued", "chunk 0 used"};
+  const char* pn_kv[7] = {"pre-pass rows", "reduction", "step flags", "first tiles issued", "first tiles landed",
+                          "chunk 0 loads issued", "chunk 0 used"};
+  // backwardQuery: 0 Q/dO fragment loads issued, 1 first K/V tile issued, 2 D summed (O read),
+  // 3 L/D stored, 4 wait_vm done, 5 barrier before the loop done.
+  const char* pn_q[7] = {"Q/dO loads issued", "first tile issued", "D summed", "L/D stored", "wait_vm done",
+                         "loop entry", ""};
+  const char* const* pn = qphase ? pn_q : pn_kv;
   for (int k = 0; k < 7; ++k) {
     std::vector<double> x;
     for (size_t w = 0; w < (1 << 14); ++w)
